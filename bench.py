@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 PyTorchTrial training throughput (samples/s, whole job).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched
+by ``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed warmup steps, then EXACTLY
+K timed steps bracketed by barrier + ``torch.cuda.synchronize()``; the max time over ranks is
+used and rank 0 prints ONE JSON line.
+
+The timed step is the full PyTorchTrial training step as run by
+``determined_amd.pytorch`` (``examples/resnet50/model_def.py:ResNet50Trial.train_batch``):
+bf16 channels-last forward/backward, bucketed RCCL all-reduce overlapped with backward,
+fused multi-tensor SGD (momentum, weight decay, fp32 master weights) -- no work skipped.
+Data: synthetic ImageNet-shaped batches (3x224x224, 1000 classes), random-init weights.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE = None  # BASELINE.json "published" is empty -> vs_baseline null
+
+
+def parse() -> argparse.Namespace:
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch size")
+    p.add_argument("--variant", default="bf16_master", choices=["bf16_master", "amp", "bf16_fp32bn"])
+    p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
+    p.add_argument("--bucket-mb", type=float, default=16.0)
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from determined_amd.benchmarks.resnet50 import build_step
+
+    step_fn, state = build_step(batch=a.batch, variant=a.variant, bucket_mb=a.bucket_mb,
+                                use_harness=not a.no_harness)
+
+    for _ in range(a.warmup):
+        step_fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step_fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    loss = float(state["last_loss"]()) if "last_loss" in state else float("nan")
+    samples = a.batch * world * a.steps
+    value = samples / dt
+    if rank == 0:
+        out = {
+            "metric": "samples/sec (whole node) + scaling eff at 1/2/4/8 MI355X, PyTorchTrial ResNet-50",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE) if BASELINE else None,
+            "dtype": "bf16",
+            "data": "synthetic (ImageNet-shaped 3x224x224, 1000 classes; random-init weights)",
+            "config": {
+                "model": "resnet50",
+                "global_batch": a.batch * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "per_gpu_batch": a.batch,
+                "variant": a.variant,
+                "harness": not a.no_harness,
+                "final_loss": round(loss, 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

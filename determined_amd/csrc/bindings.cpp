@@ -1,0 +1,263 @@
+// Python bindings for the determined_amd HIP kernels (one in-tree .so: _hip_ops).
+// Host-only translation unit: all device code lives in the *.hip files, which include
+// only hip_runtime.h so they compile in seconds; this file carries the torch headers.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace damd {
+constexpr int kMaxGroups = 8;
+struct MTChunk {
+  void* p;
+  const void* g;
+  float* s0;
+  float* s1;
+  void* p_lp;
+  int32_t n;
+  int32_t group;
+};
+struct GroupHyper {
+  float lr[kMaxGroups];
+  float wd[kMaxGroups];
+  float beta1[kMaxGroups];
+  float beta2[kMaxGroups];
+  float eps[kMaxGroups];
+  int32_t flag[kMaxGroups];
+};
+}  // namespace damd
+
+using damd::GroupHyper;
+using damd::MTChunk;
+
+// launchers (optim.hip)
+void damd_adam_launch(const void*, int, const GroupHyper&, const float*, const int32_t*, const float*, int,
+                      int, int, int, hipStream_t);
+void damd_sgd_launch(const void*, int, const GroupHyper&, const float*, const int32_t*, const float*, int,
+                     int, int, int, int, hipStream_t);
+void damd_l2norm_partial_launch(const void*, int, float*, int, hipStream_t);
+void damd_finalize_launch(const float*, int, float, const float*, float, float*, int32_t*, float*, int,
+                          hipStream_t);
+void damd_step_incr_launch(float*, const int32_t*, hipStream_t);
+void damd_scale_launch(const void*, int, const float*, int, hipStream_t);
+// launchers (norm.hip)
+void damd_norm_fwd_launch(const void*, const void*, const void*, void*, float*, float*, int64_t, int, float,
+                          int, int, int, hipStream_t);
+int damd_norm_bwd_blocks(int64_t);
+void damd_norm_bwd_launch(const void*, const void*, const float*, const float*, const void*, void*, float*,
+                          float*, int64_t, int, int, int, int, hipStream_t);
+void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+int dtype_code(const at::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return 0;
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(false, "determined_amd kernels support float32 and bfloat16 only, got ", t.scalar_type());
+}
+
+void check_cuda(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda(), what, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), what, " must be contiguous");
+}
+
+// Elementwise multi-tensor kernels only need dense storage (any memory format, e.g.
+// channels-last conv weights) with identical strides across param / grad / state.
+void check_dense_like(const at::Tensor& t, const at::Tensor& ref, const char* what) {
+  TORCH_CHECK(t.is_cuda(), what, " must be a GPU tensor");
+  TORCH_CHECK(t.is_non_overlapping_and_dense(), what, " must be dense (non-overlapping)");
+  TORCH_CHECK(t.strides() == ref.strides(), what, " strides must match the parameter's");
+}
+
+const float* opt_fptr(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_cuda(), "expected a float32 GPU tensor");
+  return t->data_ptr<float>();
+}
+int32_t* opt_iptr(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kInt && t->is_cuda(), "expected an int32 GPU tensor");
+  return t->data_ptr<int32_t>();
+}
+
+// Builds the persistent chunk table for a list of same-dtype parameters.
+// Returns a uint8 GPU tensor holding MTChunk[n_chunks]; n = numel / sizeof(MTChunk).
+at::Tensor build_chunk_table(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
+                             const std::vector<at::Tensor>& s0, const std::vector<at::Tensor>& s1,
+                             const std::vector<at::Tensor>& lp, const std::vector<int64_t>& groups,
+                             int64_t chunk_size) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && groups.size() == n, "params/grads/groups length mismatch");
+  TORCH_CHECK(s0.empty() || s0.size() == n, "state0 length mismatch");
+  TORCH_CHECK(s1.empty() || s1.size() == n, "state1 length mismatch");
+  TORCH_CHECK(lp.empty() || lp.size() == n, "low-precision copy length mismatch");
+  TORCH_CHECK(chunk_size > 0 && chunk_size % 4 == 0, "chunk_size must be a positive multiple of 4");
+  std::vector<MTChunk> table;
+  at::Device dev = at::kCPU;
+  for (size_t i = 0; i < n; ++i) {
+    const auto& p = params[i];
+    check_dense_like(p, p, "param");
+    dev = p.device();
+    const int64_t numel = p.numel();
+    TORCH_CHECK(grads[i].numel() == numel, "grad numel mismatch at index ", i);
+    check_dense_like(grads[i], p, "grad");
+    if (!s0.empty()) check_dense_like(s0[i], p, "state0");
+    if (!s1.empty()) check_dense_like(s1[i], p, "state1");
+    if (!lp.empty()) check_dense_like(lp[i], p, "low-precision param");
+    TORCH_CHECK(groups[i] >= 0 && groups[i] < damd::kMaxGroups, "group index out of range");
+    const int64_t pe = p.element_size(), ge = grads[i].element_size();
+    for (int64_t off = 0; off < numel; off += chunk_size) {
+      MTChunk c;
+      c.p = static_cast<char*>(p.data_ptr()) + off * pe;
+      c.g = static_cast<const char*>(grads[i].data_ptr()) + off * ge;
+      c.s0 = s0.empty() ? nullptr : s0[i].data_ptr<float>() + off;
+      c.s1 = s1.empty() ? nullptr : s1[i].data_ptr<float>() + off;
+      c.p_lp = lp.empty() ? nullptr : static_cast<char*>(lp[i].data_ptr()) + off * lp[i].element_size();
+      c.n = static_cast<int32_t>(std::min<int64_t>(chunk_size, numel - off));
+      c.group = static_cast<int32_t>(groups[i]);
+      table.push_back(c);
+    }
+  }
+  auto cpu = at::empty({static_cast<int64_t>(table.size() * sizeof(MTChunk))}, at::kByte);
+  if (!table.empty()) std::memcpy(cpu.data_ptr(), table.data(), table.size() * sizeof(MTChunk));
+  if (dev.is_cpu()) return cpu;
+  return cpu.to(dev);
+}
+
+int64_t chunk_entry_bytes() { return sizeof(MTChunk); }
+
+GroupHyper make_hyper(const std::vector<double>& lr, const std::vector<double>& wd,
+                      const std::vector<double>& b1, const std::vector<double>& b2,
+                      const std::vector<double>& eps, const std::vector<int64_t>& flag) {
+  GroupHyper h{};
+  TORCH_CHECK(lr.size() <= damd::kMaxGroups, "at most 8 param groups per fused launch");
+  for (size_t i = 0; i < lr.size(); ++i) {
+    h.lr[i] = static_cast<float>(lr[i]);
+    h.wd[i] = static_cast<float>(wd.at(i));
+    h.beta1[i] = static_cast<float>(b1.at(i));
+    h.beta2[i] = static_cast<float>(b2.at(i));
+    h.eps[i] = static_cast<float>(eps.at(i));
+    h.flag[i] = static_cast<int32_t>(flag.at(i));
+  }
+  return h;
+}
+
+int n_chunks_of(const at::Tensor& table) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kByte, "chunk table must be a GPU uint8 tensor");
+  return static_cast<int>(table.numel() / sizeof(MTChunk));
+}
+
+void adam_step(const at::Tensor& table, std::vector<double> lr, std::vector<double> wd, std::vector<double> b1,
+               std::vector<double> b2, std::vector<double> eps, std::vector<int64_t> decoupled,
+               const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& found_inf,
+               const at::Tensor& step, bool maximize, int64_t p_dtype, int64_t g_dtype, bool has_lp) {
+  TORCH_CHECK(step.scalar_type() == at::kFloat && step.is_cuda(), "step must be a float32 GPU scalar");
+  const GroupHyper h = make_hyper(lr, wd, b1, b2, eps, decoupled);
+  damd_adam_launch(table.data_ptr(), n_chunks_of(table), h, opt_fptr(scale), opt_iptr(found_inf),
+                   step.data_ptr<float>(), maximize, p_dtype, g_dtype, has_lp, cur_stream());
+}
+
+void sgd_step(const at::Tensor& table, std::vector<double> lr, std::vector<double> wd, std::vector<double> mom,
+              std::vector<double> damp, std::vector<int64_t> nesterov, const c10::optional<at::Tensor>& scale,
+              const c10::optional<at::Tensor>& found_inf, const at::Tensor& step, bool maximize, int64_t p_dtype,
+              int64_t g_dtype, bool has_lp, bool momentum) {
+  TORCH_CHECK(step.scalar_type() == at::kFloat && step.is_cuda(), "step must be a float32 GPU scalar");
+  std::vector<double> eps(lr.size(), 0.0);
+  const GroupHyper h = make_hyper(lr, wd, mom, damp, eps, nesterov);
+  damd_sgd_launch(table.data_ptr(), n_chunks_of(table), h, opt_fptr(scale), opt_iptr(found_inf),
+                  step.data_ptr<float>(), maximize, p_dtype, g_dtype, has_lp, momentum, cur_stream());
+}
+
+void l2norm_partial(const at::Tensor& table, at::Tensor partial, int64_t g_dtype) {
+  const int n = n_chunks_of(table);
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.numel() >= n, "partial buffer too small");
+  damd_l2norm_partial_launch(table.data_ptr(), n, partial.data_ptr<float>(), g_dtype, cur_stream());
+}
+
+void finalize(const at::Tensor& partial, int64_t n_partial, double inv_loss_scale,
+              const c10::optional<at::Tensor>& inv_scale, double max_norm, at::Tensor out,
+              const c10::optional<at::Tensor>& found_inf, const c10::optional<at::Tensor>& step, bool check_inf) {
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 2, "out must hold 2 floats");
+  float* step_ptr = nullptr;
+  if (step.has_value() && step->defined()) step_ptr = step->data_ptr<float>();
+  damd_finalize_launch(partial.data_ptr<float>(), static_cast<int>(n_partial), static_cast<float>(inv_loss_scale),
+                       opt_fptr(inv_scale), static_cast<float>(max_norm), out.data_ptr<float>(),
+                       opt_iptr(found_inf), step_ptr, check_inf, cur_stream());
+}
+
+void step_incr(at::Tensor step, const c10::optional<at::Tensor>& found_inf) {
+  damd_step_incr_launch(step.data_ptr<float>(), opt_iptr(found_inf), cur_stream());
+}
+
+void scale_grads(const at::Tensor& table, const at::Tensor& scale, int64_t g_dtype) {
+  damd_scale_launch(table.data_ptr(), n_chunks_of(table), scale.data_ptr<float>(), g_dtype, cur_stream());
+}
+
+// ----------------------------------------------------------------------------- norms
+std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& gamma, const c10::optional<at::Tensor>& beta,
+                                 double eps, bool rms) {
+  check_cuda(x, "x");
+  check_cuda(gamma, "gamma");
+  const int64_t H = gamma.numel();
+  TORCH_CHECK(x.size(-1) == H, "last dim of x must equal normalized size");
+  const int64_t rows = x.numel() / H;
+  auto y = at::empty_like(x);
+  auto opts = x.options().dtype(at::kFloat);
+  auto rstd = at::empty({rows}, opts);
+  at::Tensor mean = rms ? at::empty({0}, opts) : at::empty({rows}, opts);
+  const void* bp = nullptr;
+  if (!rms && beta.has_value() && beta->defined()) {
+    check_cuda(*beta, "beta");
+    TORCH_CHECK(beta->scalar_type() == gamma.scalar_type(), "beta dtype must match gamma");
+    bp = beta->data_ptr();
+  }
+  if (rows > 0)
+    damd_norm_fwd_launch(x.data_ptr(), gamma.data_ptr(), bp, y.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
+                         rstd.data_ptr<float>(), rows, static_cast<int>(H), static_cast<float>(eps), rms,
+                         dtype_code(x), dtype_code(gamma), cur_stream());
+  return {y, mean, rstd};
+}
+
+std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean,
+                                 const at::Tensor& rstd, const at::Tensor& gamma, bool rms) {
+  check_cuda(dy, "dy");
+  check_cuda(x, "x");
+  const int64_t H = gamma.numel();
+  const int64_t rows = x.numel() / H;
+  auto dx = at::empty_like(x);
+  auto fopts = x.options().dtype(at::kFloat);
+  auto dgamma = at::zeros({H}, fopts);
+  auto dbeta = rms ? at::empty({0}, fopts) : at::zeros({H}, fopts);
+  if (rows > 0) {
+    const int W = damd_norm_bwd_blocks(rows) * 4;
+    auto part_g = at::empty({W, H}, fopts);
+    auto part_b = rms ? at::empty({0}, fopts) : at::empty({W, H}, fopts);
+    damd_norm_bwd_launch(dy.data_ptr(), x.data_ptr(), rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         gamma.data_ptr(), dx.data_ptr(), part_g.data_ptr<float>(),
+                         rms ? nullptr : part_b.data_ptr<float>(), rows, static_cast<int>(H), rms, dtype_code(x),
+                         dtype_code(gamma), cur_stream());
+    damd_col_reduce_launch(part_g.data_ptr<float>(), dgamma.data_ptr<float>(), W, static_cast<int>(H), cur_stream());
+    if (!rms)
+      damd_col_reduce_launch(part_b.data_ptr<float>(), dbeta.data_ptr<float>(), W, static_cast<int>(H),
+                             cur_stream());
+  }
+  return {dx, dgamma, dbeta};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "determined_amd CDNA4 HIP kernels";
+  m.def("build_chunk_table", &build_chunk_table);
+  m.def("chunk_entry_bytes", &chunk_entry_bytes);
+  m.def("adam_step", &adam_step);
+  m.def("sgd_step", &sgd_step);
+  m.def("l2norm_partial", &l2norm_partial);
+  m.def("finalize", &finalize);
+  m.def("step_incr", &step_incr);
+  m.def("scale_grads", &scale_grads);
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+}

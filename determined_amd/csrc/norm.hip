@@ -1,0 +1,358 @@
+// LayerNorm / RMSNorm forward + backward for CDNA4 (gfx950).
+//
+// Layout: x is [rows, H] row-major. One 64-lane wave owns one row; lane l owns the
+// 8-element (16 B for bf16) vectors l, l+64, l+128, ... so every wave-instruction moves
+// a contiguous 1 KiB (bf16) / 2 KiB (fp32) span. For H <= 64*8*NV the row lives in
+// registers (NV vectors per lane) and is read from HBM exactly once; the variance is a
+// true two-pass over registers (no E[x^2]-E[x]^2 cancellation).
+//
+// Backward: dx in the same row-per-wave pass; dgamma/dbeta are accumulated in
+// registers across all rows a wave visits (grid-stride) and written once per wave
+// as fp32 partials, then reduced by a column kernel — no per-row atomics.
+// (Reference counterpart: apex/torch fused LayerNorm used by the HF/DeepSpeed paths.)
+
+#include "common.h"
+
+namespace damd {
+
+constexpr int kNormThreads = 256;  // 4 waves = 4 rows in flight per block
+constexpr int kVecElems = 8;
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+  static __device__ __forceinline__ void ld(const bf16_t* p, float* o) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = bf2f(r.v[k]);
+  }
+  static __device__ __forceinline__ void st(bf16_t* p, const float* o) {
+    bf16x8 r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = f2bf(o[k]);
+    *reinterpret_cast<bf16x8*>(p) = r;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void ld(const float* p, float* o) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float* o) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+};
+
+// ------------------------------------------------------------------ forward (register-resident)
+template <typename T, typename WT, int NV, bool RMS>
+__global__ void __launch_bounds__(kNormThreads)
+norm_fwd_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, const WT* __restrict__ beta,
+                T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
+  if (row >= rows) return;
+  const T* xr = x + row * H;
+  float v[NV][kVecElems];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * kWave + lane) * kVecElems;
+    if (c < H) {
+      Vec8<T>::ld(xr + c, v[j]);
+#pragma unroll
+      for (int k = 0; k < kVecElems; ++k) s += v[j][k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kVecElems; ++k) v[j][k] = 0.f;
+    }
+  }
+  const float invH = 1.f / static_cast<float>(H);
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(s) * invH;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * kWave + lane) * kVecElems;
+    if (c < H) {
+#pragma unroll
+      for (int k = 0; k < kVecElems; ++k) { const float d = v[j][k] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) * invH + eps);
+  T* yr = y + row * H;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * kWave + lane) * kVecElems;
+    if (c < H) {
+      float gw[kVecElems], bw[kVecElems], o[kVecElems];
+      Vec8<WT>::ld(gamma + c, gw);
+      if (!RMS && beta != nullptr) Vec8<WT>::ld(beta + c, bw);
+#pragma unroll
+      for (int k = 0; k < kVecElems; ++k) {
+        o[k] = (v[j][k] - mean) * rstd * gw[k];
+        if (!RMS && beta != nullptr) o[k] += bw[k];
+      }
+      Vec8<T>::st(yr + c, o);
+    }
+  }
+  if (lane == 0) {
+    if (!RMS && mean_out) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// ------------------------------------------------------------------ forward (generic H, 2 reads)
+template <typename T, typename WT, bool RMS>
+__global__ void __launch_bounds__(kNormThreads)
+norm_fwd_generic_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, const WT* __restrict__ beta,
+                        T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                        int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
+  if (row >= rows) return;
+  const T* xr = x + row * H;
+  float s = 0.f;
+  for (int c = lane; c < H; c += kWave) s += Elem<T>::ld(xr, c);
+  const float invH = 1.f / static_cast<float>(H);
+  const float mean = RMS ? 0.f : wave_sum(s) * invH;
+  float q = 0.f;
+  for (int c = lane; c < H; c += kWave) { const float d = Elem<T>::ld(xr, c) - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) * invH + eps);
+  T* yr = y + row * H;
+  for (int c = lane; c < H; c += kWave) {
+    float o = (Elem<T>::ld(xr, c) - mean) * rstd * Elem<WT>::ld(gamma, c);
+    if (!RMS && beta != nullptr) o += Elem<WT>::ld(beta, c);
+    Elem<T>::st(yr, c, o);
+  }
+  if (lane == 0) {
+    if (!RMS && mean_out) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// ------------------------------------------------------------------ backward (register-resident)
+// part_g / part_b: [n_waves_total, H] fp32 partials for dgamma / dbeta.
+template <typename T, typename WT, int NV, bool RMS>
+__global__ void __launch_bounds__(kNormThreads)
+norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean_in,
+                const float* __restrict__ rstd_in, const WT* __restrict__ gamma, T* __restrict__ dx,
+                float* __restrict__ part_g, float* __restrict__ part_b, int64_t rows, int H) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave_id = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
+  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * (kNormThreads / kWave);
+  float ag[NV][kVecElems], ab[NV][kVecElems], gw[NV][kVecElems];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * kWave + lane) * kVecElems;
+#pragma unroll
+    for (int k = 0; k < kVecElems; ++k) { ag[j][k] = 0.f; ab[j][k] = 0.f; gw[j][k] = 0.f; }
+    if (c < H) Vec8<WT>::ld(gamma + c, gw[j]);
+  }
+  const float invH = 1.f / static_cast<float>(H);
+  for (int64_t row = wave_id; row < rows; row += n_waves) {
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[NV][kVecElems], g[NV][kVecElems];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * kWave + lane) * kVecElems;
+      if (c < H) {
+        float xv[kVecElems];
+        Vec8<T>::ld(x + row * H + c, xv);
+        Vec8<T>::ld(dy + row * H + c, g[j]);
+#pragma unroll
+        for (int k = 0; k < kVecElems; ++k) {
+          xh[j][k] = (xv[k] - mean) * rstd;
+          ag[j][k] += g[j][k] * xh[j][k];
+          ab[j][k] += g[j][k];
+          const float wdy = g[j][k] * gw[j][k];
+          s1 += wdy * xh[j][k];
+          s2 += wdy;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kVecElems; ++k) { xh[j][k] = 0.f; g[j][k] = 0.f; }
+      }
+    }
+    const float c1 = wave_sum(s1) * invH;
+    const float c2 = RMS ? 0.f : wave_sum(s2) * invH;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * kWave + lane) * kVecElems;
+      if (c < H) {
+        float o[kVecElems];
+#pragma unroll
+        for (int k = 0; k < kVecElems; ++k)
+          o[k] = rstd * (g[j][k] * gw[j][k] - xh[j][k] * c1 - c2);
+        Vec8<T>::st(dx + row * H + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * kWave + lane) * kVecElems;
+    if (c < H) {
+      Vec8<float>::st(part_g + wave_id * H + c, ag[j]);
+      if (!RMS) Vec8<float>::st(part_b + wave_id * H + c, ab[j]);
+    }
+  }
+}
+
+template <typename T, typename WT, bool RMS>
+__global__ void __launch_bounds__(kNormThreads)
+norm_bwd_generic_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean_in,
+                        const float* __restrict__ rstd_in, const WT* __restrict__ gamma, T* __restrict__ dx,
+                        float* __restrict__ part_g, float* __restrict__ part_b, int64_t rows, int H) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave_id = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
+  const int64_t n_waves = static_cast<int64_t>(gridDim.x) * (kNormThreads / kWave);
+  for (int c = lane; c < H; c += kWave) {
+    part_g[wave_id * H + c] = 0.f;
+    if (!RMS) part_b[wave_id * H + c] = 0.f;
+  }
+  const float invH = 1.f / static_cast<float>(H);
+  for (int64_t row = wave_id; row < rows; row += n_waves) {
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    const T* xr = x + row * H;
+    const T* dyr = dy + row * H;
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = lane; c < H; c += kWave) {
+      const float xh = (Elem<T>::ld(xr, c) - mean) * rstd;
+      const float g = Elem<T>::ld(dyr, c);
+      const float wdy = g * Elem<WT>::ld(gamma, c);
+      s1 += wdy * xh; s2 += wdy;
+      part_g[wave_id * H + c] += g * xh;
+      if (!RMS) part_b[wave_id * H + c] += g;
+    }
+    const float c1 = wave_sum(s1) * invH;
+    const float c2 = RMS ? 0.f : wave_sum(s2) * invH;
+    for (int c = lane; c < H; c += kWave) {
+      const float xh = (Elem<T>::ld(xr, c) - mean) * rstd;
+      const float wdy = Elem<T>::ld(dyr, c) * Elem<WT>::ld(gamma, c);
+      Elem<T>::st(dx + row * H, c, rstd * (wdy - xh * c1 - c2));
+    }
+  }
+}
+
+// Column reduction of [W, H] partials -> out[H] (fp32, pre-zeroed). grid = (ceil(H/64), S).
+__global__ void __launch_bounds__(256)
+col_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int W, int H) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;  // 0..3
+  const int slice = (W + gridDim.y - 1) / gridDim.y;
+  const int w0 = blockIdx.y * slice, w1 = min(W, w0 + slice);
+  float acc = 0.f;
+  if (col < H)
+    for (int w = w0 + rl; w < w1; w += 4) acc += part[static_cast<int64_t>(w) * H + col];
+  red[rl][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rl == 0 && col < H) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + col, s);
+  }
+}
+
+}  // namespace damd
+
+using namespace damd;
+
+namespace {
+template <typename T, typename WT, bool RMS>
+void fwd_dispatch(const void* x, const void* g, const void* b, void* y, float* mean, float* rstd,
+                  int64_t rows, int H, float eps, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>((rows + 3) / 4)), block(kNormThreads);
+  const T* xp = static_cast<const T*>(x);
+  const WT* gp = static_cast<const WT*>(g);
+  const WT* bp = static_cast<const WT*>(b);
+  T* yp = static_cast<T*>(y);
+  const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
+  const bool vec_ok = (H % kVecElems) == 0 && nv <= 16;
+#define FWD_NV(N) hipLaunchKernelGGL((norm_fwd_kernel<T, WT, N, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps)
+  if (vec_ok) {
+    switch (nv) {
+      case 1: FWD_NV(1); break;
+      case 2: FWD_NV(2); break;
+      case 3: FWD_NV(3); break;
+      case 4: FWD_NV(4); break;
+      case 5: case 6: FWD_NV(6); break;
+      case 7: case 8: FWD_NV(8); break;
+      default: FWD_NV(16); break;
+    }
+  } else {
+    hipLaunchKernelGGL((norm_fwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps);
+  }
+#undef FWD_NV
+  DAMD_CHECK_LAUNCH();
+}
+
+template <typename T, typename WT, bool RMS>
+void bwd_dispatch(const void* dy, const void* x, const float* mean, const float* rstd, const void* g,
+                  void* dx, float* part_g, float* part_b, int64_t rows, int H, int n_blocks,
+                  hipStream_t st) {
+  const dim3 grid(n_blocks), block(kNormThreads);
+  const T* dyp = static_cast<const T*>(dy);
+  const T* xp = static_cast<const T*>(x);
+  const WT* gp = static_cast<const WT*>(g);
+  T* dxp = static_cast<T*>(dx);
+  const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
+  const bool vec_ok = (H % kVecElems) == 0 && nv <= 4;  // 5*NV*8 live fp32 regs
+#define BWD_NV(N) hipLaunchKernelGGL((norm_bwd_kernel<T, WT, N, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H)
+  if (vec_ok) {
+    switch (nv) {
+      case 1: BWD_NV(1); break;
+      case 2: BWD_NV(2); break;
+      default: BWD_NV(4); break;
+    }
+  } else {
+    hipLaunchKernelGGL((norm_bwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H);
+  }
+#undef BWD_NV
+  DAMD_CHECK_LAUNCH();
+}
+}  // namespace
+
+// dtype codes: 0 = fp32, 1 = bf16
+void damd_norm_fwd_launch(const void* x, const void* gamma, const void* beta, void* y, float* mean,
+                          float* rstd, int64_t rows, int H, float eps, int rms, int x_dtype,
+                          int w_dtype, hipStream_t st) {
+#define FD(T, WT) do { if (rms) fwd_dispatch<T, WT, true>(x, gamma, beta, y, mean, rstd, rows, H, eps, st); \
+                       else fwd_dispatch<T, WT, false>(x, gamma, beta, y, mean, rstd, rows, H, eps, st); } while (0)
+  if (x_dtype == 1 && w_dtype == 1) FD(bf16_t, bf16_t);
+  else if (x_dtype == 1) FD(bf16_t, float);
+  else if (w_dtype == 1) FD(float, bf16_t);
+  else FD(float, float);
+#undef FD
+}
+
+// Number of blocks used by the backward grid (=> partial rows = 4 * blocks).
+int damd_norm_bwd_blocks(int64_t rows) {
+  int64_t b = (rows + 3) / 4;
+  if (b > 512) b = 512;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+void damd_norm_bwd_launch(const void* dy, const void* x, const float* mean, const float* rstd,
+                          const void* gamma, void* dx, float* part_g, float* part_b, int64_t rows,
+                          int H, int rms, int x_dtype, int w_dtype, hipStream_t st) {
+  const int nb = damd_norm_bwd_blocks(rows);
+#define BD(T, WT) do { if (rms) bwd_dispatch<T, WT, true>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); \
+                       else bwd_dispatch<T, WT, false>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); } while (0)
+  if (x_dtype == 1 && w_dtype == 1) BD(bf16_t, bf16_t);
+  else if (x_dtype == 1) BD(bf16_t, float);
+  else if (w_dtype == 1) BD(float, bf16_t);
+  else BD(float, float);
+#undef BD
+}
+
+void damd_col_reduce_launch(const float* part, float* out, int W, int H, hipStream_t st) {
+  int S = W / 64;
+  if (S < 1) S = 1;
+  if (S > 32) S = 32;
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64, S), dim3(256), 0, st, part, out, W, H);
+  DAMD_CHECK_LAUNCH();
+}

@@ -1,0 +1,73 @@
+"""Hand-written CDNA4 (gfx950) HIP kernels and their torch-facing wrappers.
+
+The kernels live in ``determined_amd/csrc`` and are compiled in-tree into
+``determined_amd/ops/_hip_ops*.so`` by ``determined_amd._build`` (driven from
+``__graft_entry__.build``).  GPU tensors ALWAYS go through the HIP path: if the
+extension is missing on a machine with a GPU the call raises instead of silently
+falling back.  CPU tensors use an exact PyTorch reference implementation of the same
+math (that is what the CPU test-suite exercises).
+"""
+
+import importlib
+import os
+from typing import Any, Optional
+
+_ext: Optional[Any] = None
+_err: Optional[BaseException] = None
+
+
+def _load() -> Optional[Any]:
+    global _ext, _err
+    if _ext is not None or _err is not None:
+        return _ext
+    try:
+        import torch  # noqa: F401  (loads libtorch/libamdhip64 before the extension)
+
+        _ext = importlib.import_module("determined_amd.ops._hip_ops")
+    except BaseException as e:  # ImportError, OSError from a bad .so, ...
+        _err = e
+        if os.environ.get("DAMD_AUTOBUILD", "0") == "1":
+            from determined_amd import _build
+
+            _build.build_hip_ops()
+            _err = None
+            _ext = importlib.import_module("determined_amd.ops._hip_ops")
+    return _ext
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def ext() -> Any:
+    """Return the compiled extension or raise loudly (used for every GPU tensor)."""
+    e = _load()
+    if e is None:
+        raise RuntimeError(
+            "determined_amd HIP kernels are not built (run `python -m determined_amd._build`); "
+            f"import error: {_err!r}"
+        )
+    return e
+
+
+from determined_amd.ops.optim import FusedAdamW, FusedSGD, fused_clip_grad_norm_  # noqa: E402
+from determined_amd.ops.norm import (  # noqa: E402
+    FusedLayerNorm,
+    FusedRMSNorm,
+    layer_norm,
+    rms_norm,
+)
+from determined_amd.ops.scaler import DeviceGradScaler  # noqa: E402
+
+__all__ = [
+    "available",
+    "ext",
+    "FusedAdamW",
+    "FusedSGD",
+    "fused_clip_grad_norm_",
+    "FusedLayerNorm",
+    "FusedRMSNorm",
+    "layer_norm",
+    "rms_norm",
+    "DeviceGradScaler",
+]

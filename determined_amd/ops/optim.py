@@ -1,0 +1,456 @@
+"""Multi-tensor fused optimizers (AdamW / SGD) backed by the CDNA4 kernels in csrc/optim.hip.
+
+Design (MI355X-first, not a per-parameter loop):
+
+* A persistent chunk table describing every (param, grad, state) tensor is built once
+  and cached on the device; it is rebuilt only if a tensor's storage moves.  Each step
+  is then at most three kernel launches for the whole model, independent of parameter
+  count: grad-norm partials -> finalize (clip coefficient, AMP unscale, inf check,
+  device step counter) -> update.
+* Nothing in ``step()`` synchronises with the host: the step counter, the clip
+  coefficient and ``found_inf`` all live in device memory.
+* ``master_weights=True`` keeps an fp32 master copy for bf16 parameters and writes the
+  rounded bf16 value back in the same pass (bf16 forward/backward + fp32 update).
+
+Reference semantics: ``torch.optim.AdamW`` / ``torch.optim.SGD``; the fused clip replaces
+``torch.nn.utils.clip_grad_norm_`` used by ``PyTorchTrialContext.step_optimizer``
+(reference ``harness/determined/pytorch/_pytorch_context.py:814``).
+"""
+
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
+
+import torch
+
+from determined_amd.utils.tensor import is_dense
+
+CHUNK = 16384
+MAX_GROUPS = 8
+
+
+def _dcode(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise TypeError(f"fused optimizers support float32/bfloat16 tensors, got {t.dtype}")
+
+
+class _Plan:
+    __slots__ = ("key", "table", "n_chunks", "p_dtype", "g_dtype", "has_lp", "groups")
+
+    def __init__(self, key, table, n_chunks, p_dtype, g_dtype, has_lp, groups):
+        self.key = key
+        self.table = table
+        self.n_chunks = n_chunks
+        self.p_dtype = p_dtype
+        self.g_dtype = g_dtype
+        self.has_lp = has_lp
+        self.groups = groups
+
+
+def _ptrs(ts: List[torch.Tensor]) -> Tuple[int, ...]:
+    return tuple(t.data_ptr() for t in ts)
+
+
+def _build_plan(
+    params: List[torch.Tensor],
+    grads: List[torch.Tensor],
+    s0: List[torch.Tensor],
+    s1: List[torch.Tensor],
+    lp: List[torch.Tensor],
+    groups: List[int],
+    key: Any,
+) -> _Plan:
+    from determined_amd import ops
+
+    e = ops.ext()
+    table = e.build_chunk_table(params, grads, s0, s1, lp, groups, CHUNK)
+    n = table.numel() // e.chunk_entry_bytes()
+    return _Plan(key, table, n, _dcode(params[0]), _dcode(grads[0]), bool(lp), groups)
+
+
+class _FusedBase(torch.optim.Optimizer):
+    """Shared plumbing: bucketing by dtype, plan cache, device step counter, fused clip."""
+
+    _state_keys: Tuple[str, ...] = ()
+
+    def __init__(self, params: Iterable, defaults: Dict[str, Any], master_weights: bool) -> None:
+        super().__init__(params, defaults)
+        self.master_weights = master_weights
+        self._plans: Dict[Any, _Plan] = {}
+        self._step_t: Dict[torch.device, torch.Tensor] = {}
+        self._aux: Dict[torch.device, Dict[str, torch.Tensor]] = {}
+        self.max_grad_norm: Optional[float] = None
+        self.last_grad_norm: Optional[torch.Tensor] = None
+
+    # -- step counter --------------------------------------------------------------------
+    def _step_tensor(self, device: torch.device) -> torch.Tensor:
+        t = self._step_t.get(device)
+        if t is None:
+            init = 0.0
+            for group in self.param_groups:
+                for p in group["params"]:
+                    st = self.state.get(p, {})
+                    if "step" in st:
+                        init = float(st["step"])
+                        break
+            t = torch.full((1,), init, dtype=torch.float32, device=device)
+            self._step_t[device] = t
+        return t
+
+    def _aux_buffers(self, device: torch.device, n_partial: int) -> Dict[str, torch.Tensor]:
+        a = self._aux.get(device)
+        if a is None or a["partial"].numel() < n_partial:
+            a = {
+                "partial": torch.empty(max(n_partial, 1), dtype=torch.float32, device=device),
+                "out": torch.empty(2, dtype=torch.float32, device=device),
+                "found_inf": torch.zeros(1, dtype=torch.int32, device=device),
+            }
+            self._aux[device] = a
+        return a
+
+    def set_grad_clipping(self, max_norm: Optional[float]) -> None:
+        """Fuse clip-by-global-norm into step() (no extra pass over gradients)."""
+        self.max_grad_norm = None if max_norm is None or max_norm <= 0 else float(max_norm)
+
+    # -- state ---------------------------------------------------------------------------
+    def _init_state(self, p: torch.Tensor, state: Dict[str, Any]) -> None:
+        raise NotImplementedError
+
+    def _master(self, p: torch.Tensor, state: Dict[str, Any]) -> Optional[torch.Tensor]:
+        if self.master_weights and p.dtype == torch.bfloat16:
+            if "master" not in state:
+                state["master"] = p.detach().float().clone()
+            return state["master"]
+        return None
+
+    def _gpu_buckets(self) -> Dict[Any, Dict[str, list]]:
+        buckets: Dict[Any, Dict[str, list]] = {}
+        for gi, group in enumerate(self.param_groups):
+            batch = gi // MAX_GROUPS
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("fused optimizers do not support sparse gradients")
+                state = self.state[p]
+                if not state:
+                    self._init_state(p, state)
+                master = self._master(p, state)
+                tgt = master if master is not None else p
+                key = (p.device, batch, _dcode(tgt), _dcode(p.grad), master is not None)
+                b = buckets.setdefault(key, {"p": [], "g": [], "s0": [], "s1": [], "lp": [], "grp": []})
+                b["p"].append(tgt)
+                b["g"].append(p.grad)
+                sts = [state[k] for k in self._state_keys]
+                if len(sts) > 0:
+                    b["s0"].append(sts[0])
+                if len(sts) > 1:
+                    b["s1"].append(sts[1])
+                if master is not None:
+                    b["lp"].append(p)
+                b["grp"].append(gi % MAX_GROUPS)
+        return buckets
+
+    def _plan_for(self, key: Any, b: Dict[str, list]) -> _Plan:
+        ck = (key, _ptrs(b["p"]), _ptrs(b["g"]), _ptrs(b["s0"]), _ptrs(b["s1"]), _ptrs(b["lp"]))
+        plan = self._plans.get(key)
+        if plan is None or plan.key != ck:
+            for p, g in zip(b["p"], b["g"]):
+                if g.stride() != p.stride() or not is_dense(g):
+                    raise RuntimeError("fused optimizers require dense grads laid out like their params")
+            plan = _build_plan(b["p"], b["g"], b["s0"], b["s1"], b["lp"], b["grp"], ck)
+            self._plans[key] = plan
+        return plan
+
+    def _group_hyper(self, batch: int) -> List[Dict[str, Any]]:
+        return self.param_groups[batch * MAX_GROUPS : (batch + 1) * MAX_GROUPS]
+
+    def _launch(self, plan: _Plan, hyper: List[Dict[str, Any]], scale, found_inf, step_t) -> None:
+        raise NotImplementedError
+
+    def _cpu_update(self, p: torch.Tensor, group: Dict[str, Any], state: Dict[str, Any], gscale: float) -> None:
+        raise NotImplementedError
+
+    @torch.no_grad()
+    def step(
+        self,
+        closure: Optional[Callable[[], float]] = None,
+        grad_scale: Optional[torch.Tensor] = None,
+        found_inf: Optional[torch.Tensor] = None,
+        inv_loss_scale: float = 1.0,
+        check_finite: bool = False,
+    ) -> Optional[float]:
+        """One optimizer step.
+
+        ``grad_scale`` (device fp32 scalar) multiplies every gradient (AMP unscale);
+        ``found_inf`` (device int32 scalar) skips the update entirely when non-zero.
+        ``check_finite`` runs the norm pass to detect inf/nan (written into ``found_inf``).
+        """
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        cpu_params = [p for g in self.param_groups for p in g["params"] if p.grad is not None and not p.is_cuda]
+        if cpu_params:
+            self._cpu_step(inv_loss_scale, grad_scale, found_inf)
+            return loss
+        from determined_amd import ops
+
+        e = ops.ext()
+        buckets = self._gpu_buckets()
+        by_dev: Dict[torch.device, List[Tuple[Any, _Plan]]] = {}
+        for key, b in buckets.items():
+            by_dev.setdefault(key[0], []).append((key, self._plan_for(key, b)))
+        for dev, plans in by_dev.items():
+            step_t = self._step_tensor(dev)
+            need_norm = self.max_grad_norm is not None or check_finite
+            scale_t = grad_scale
+            fi = found_inf
+            if need_norm:
+                total = sum(pl.n_chunks for _, pl in plans)
+                aux = self._aux_buffers(dev, total)
+                off = 0
+                for _, pl in plans:
+                    e.l2norm_partial(pl.table, aux["partial"][off : off + pl.n_chunks], pl.g_dtype)
+                    off += pl.n_chunks
+                fi = found_inf if found_inf is not None else aux["found_inf"]
+                # finalize also advances the device step counter unless overflow.
+                # finalize: clip coefficient x inv loss scale, found_inf, and the device
+                # step counter (not advanced on overflow).
+                e.finalize(
+                    aux["partial"], total, inv_loss_scale, grad_scale, self.max_grad_norm or 0.0,
+                    aux["out"], fi, step_t, True,
+                )
+                scale_t = aux["out"][0:1]
+                self.last_grad_norm = aux["out"][1:2]
+            else:
+                if grad_scale is None and inv_loss_scale != 1.0:
+                    scale_t = torch.full((1,), inv_loss_scale, dtype=torch.float32, device=dev)
+                e.step_incr(step_t, fi)
+            for key, pl in plans:
+                self._launch(pl, self._group_hyper(key[1]), scale_t, fi, step_t)
+        return loss
+
+    # -- CPU reference path (exact same math, used off-GPU) --------------------------------
+    @torch.no_grad()
+    def _cpu_step(self, inv_loss_scale: float, grad_scale, found_inf) -> None:
+        if found_inf is not None and int(found_inf.item()) != 0:
+            return
+        gscale = inv_loss_scale * (float(grad_scale.item()) if grad_scale is not None else 1.0)
+        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if self.max_grad_norm is not None and params:
+            norm = torch.sqrt(sum((p.grad.float() ** 2).sum() for p in params)) * gscale
+            self.last_grad_norm = norm.reshape(1)
+            if not torch.isfinite(norm):
+                return
+            gscale *= min(1.0, self.max_grad_norm / (float(norm) + 1e-6))
+        dev = params[0].device if params else torch.device("cpu")
+        step_t = self._step_tensor(dev)
+        step_t += 1
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                state = self.state[p]
+                if not state:
+                    self._init_state(p, state)
+                self._cpu_update(p, group, state, gscale)
+
+    def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
+        super().load_state_dict(state_dict)
+        self._plans.clear()
+        self._step_t.clear()
+        # Re-share one step tensor per device across params (state["step"]).
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    dev = p.device
+                    t = self._step_tensor(dev)
+                    st["step"] = t
+                    for k in self._state_keys:
+                        if k in st and st[k].dtype != torch.float32:
+                            st[k] = st[k].float()
+
+
+class FusedAdamW(_FusedBase):
+    """AdamW (``adam_w_mode=True``, decoupled decay) or Adam (L2 decay) in one fused launch."""
+
+    _state_keys = ("exp_avg", "exp_avg_sq")
+
+    def __init__(
+        self,
+        params: Iterable,
+        lr: float = 1e-3,
+        betas: Tuple[float, float] = (0.9, 0.999),
+        eps: float = 1e-8,
+        weight_decay: float = 1e-2,
+        adam_w_mode: bool = True,
+        maximize: bool = False,
+        master_weights: bool = False,
+    ) -> None:
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adam_w_mode=adam_w_mode,
+                        maximize=maximize)
+        super().__init__(params, defaults, master_weights)
+
+    def _init_state(self, p: torch.Tensor, state: Dict[str, Any]) -> None:
+        state["step"] = self._step_tensor(p.device)
+        state["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+        state["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+
+    def _launch(self, plan, hyper, scale, found_inf, step_t) -> None:
+        from determined_amd import ops
+
+        ops.ext().adam_step(
+            plan.table,
+            [float(g["lr"]) for g in hyper],
+            [float(g["weight_decay"]) for g in hyper],
+            [float(g["betas"][0]) for g in hyper],
+            [float(g["betas"][1]) for g in hyper],
+            [float(g["eps"]) for g in hyper],
+            [int(bool(g.get("adam_w_mode", True))) for g in hyper],
+            scale,
+            found_inf,
+            step_t,
+            bool(hyper[0].get("maximize", False)),
+            plan.p_dtype,
+            plan.g_dtype,
+            plan.has_lp,
+        )
+
+    def _cpu_update(self, p, group, state, gscale) -> None:
+        step = float(self._step_tensor(p.device).item())
+        b1, b2 = group["betas"]
+        lr, wd, eps = group["lr"], group["weight_decay"], group["eps"]
+        master = self._master(p, state)
+        w = master if master is not None else p.data.float()
+        g = p.grad.float() * gscale
+        if group.get("maximize", False):
+            g = -g
+        if group.get("adam_w_mode", True):
+            w = w * (1 - lr * wd)
+        else:
+            g = g + wd * w
+        m, v = state["exp_avg"], state["exp_avg_sq"]
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1**step
+        bc2 = 1 - b2**step
+        denom = v.sqrt() / (bc2**0.5) + eps
+        w = w - (lr / bc1) * m / denom
+        if master is not None:
+            master.copy_(w)
+        p.data.copy_(w.to(p.dtype))
+
+
+class FusedSGD(_FusedBase):
+    """SGD with momentum / dampening / nesterov / weight decay in one fused launch."""
+
+    _state_keys = ("momentum_buffer",)
+
+    def __init__(
+        self,
+        params: Iterable,
+        lr: float = 1e-3,
+        momentum: float = 0.0,
+        dampening: float = 0.0,
+        weight_decay: float = 0.0,
+        nesterov: bool = False,
+        maximize: bool = False,
+        master_weights: bool = False,
+    ) -> None:
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov, maximize=maximize)
+        super().__init__(params, defaults, master_weights)
+        self._state_keys = ("momentum_buffer",) if any(g["momentum"] != 0 for g in self.param_groups) else ()
+
+    def _init_state(self, p: torch.Tensor, state: Dict[str, Any]) -> None:
+        state["step"] = self._step_tensor(p.device)
+        if self._state_keys:
+            state["momentum_buffer"] = torch.zeros_like(p, dtype=torch.float32,
+                                                        memory_format=torch.preserve_format)
+
+    def _launch(self, plan, hyper, scale, found_inf, step_t) -> None:
+        from determined_amd import ops
+
+        ops.ext().sgd_step(
+            plan.table,
+            [float(g["lr"]) for g in hyper],
+            [float(g["weight_decay"]) for g in hyper],
+            [float(g["momentum"]) for g in hyper],
+            [float(g["dampening"]) for g in hyper],
+            [int(bool(g["nesterov"])) for g in hyper],
+            scale,
+            found_inf,
+            step_t,
+            bool(hyper[0].get("maximize", False)),
+            plan.p_dtype,
+            plan.g_dtype,
+            plan.has_lp,
+            bool(self._state_keys),
+        )
+
+    def _cpu_update(self, p, group, state, gscale) -> None:
+        step = float(self._step_tensor(p.device).item())
+        master = self._master(p, state)
+        w = master if master is not None else p.data.float()
+        g = p.grad.float() * gscale
+        if group.get("maximize", False):
+            g = -g
+        g = g + group["weight_decay"] * w
+        mom = group["momentum"]
+        if mom != 0:
+            buf = state["momentum_buffer"]
+            if step <= 1:
+                buf.copy_(g)
+            else:
+                buf.mul_(mom).add_(g, alpha=1 - group["dampening"])
+            g = g + mom * buf if group["nesterov"] else buf
+        w = w - group["lr"] * g
+        if master is not None:
+            master.copy_(w)
+        p.data.copy_(w.to(p.dtype))
+
+
+@torch.no_grad()
+def fused_clip_grad_norm_(
+    parameters: Iterable[torch.Tensor], max_norm: float, error_if_nonfinite: bool = False
+) -> torch.Tensor:
+    """Drop-in for ``torch.nn.utils.clip_grad_norm_`` (L2): 3 launches per dtype, no host sync.
+
+    Returns the total norm as a device tensor.
+    """
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.zeros(())
+    if not params[0].is_cuda:
+        return torch.nn.utils.clip_grad_norm_(params, max_norm, error_if_nonfinite=error_if_nonfinite)
+    from determined_amd import ops
+
+    e = ops.ext()
+    dev = params[0].device
+    by_dt: Dict[torch.dtype, List[torch.Tensor]] = {}
+    for p in params:
+        by_dt.setdefault(p.grad.dtype, []).append(p.grad)
+    plans = []
+    for dt, gs in by_dt.items():
+        if not all(is_dense(g) for g in gs):
+            return torch.nn.utils.clip_grad_norm_(params, max_norm, error_if_nonfinite=error_if_nonfinite)
+        plans.append(_build_plan(gs, gs, [], [], [], [0] * len(gs), None))
+    total = sum(pl.n_chunks for pl in plans)
+    partial = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    off = 0
+    for pl in plans:
+        e.l2norm_partial(pl.table, partial[off : off + pl.n_chunks], pl.g_dtype)
+        off += pl.n_chunks
+    e.finalize(partial, total, 1.0, None, float(max_norm), out, None, None, False)
+    for pl in plans:
+        e.scale_grads(pl.table, out[0:1], pl.g_dtype)
+    norm = out[1]
+    if error_if_nonfinite and not bool(torch.isfinite(norm)):
+        raise RuntimeError("The total norm of gradients is non-finite")
+    return norm

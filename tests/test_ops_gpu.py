@@ -1,0 +1,196 @@
+"""Numerics of the hand-written HIP kernels vs plain PyTorch fp32 references (run on MI355X)."""
+
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import determined_amd.ops as ops
+
+    ops.ext()  # must load: these tests exist to exercise the native path
+    return ops
+
+
+def _params(shapes, dtype=torch.float32, seed=0):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda", generator=g).to(dtype)) for s in shapes]
+    for p in ps:
+        p.grad = torch.randn(p.shape, device="cuda", generator=g).to(dtype)
+    return ps
+
+
+SHAPES = [(3,), (17, 5), (1024,), (64, 3, 7, 7), (257, 129), (40000,)]
+
+
+@pytest.mark.parametrize("adam_w_mode", [True, False])
+def test_fused_adamw_matches_torch(ops, adam_w_mode):
+    ref = _params(SHAPES)
+    ours = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    for a, b in zip(ours, ref):
+        a.grad = b.grad.clone()
+    Ref = torch.optim.AdamW if adam_w_mode else torch.optim.Adam
+    o_ref = Ref(ref, lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.1)
+    o_ours = ops.FusedAdamW(ours, lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.1, adam_w_mode=adam_w_mode)
+    for step in range(5):
+        for a, b in zip(ours, ref):
+            g = torch.randn_like(b) * (step + 1)
+            a.grad.copy_(g)
+            b.grad.copy_(g)
+        o_ref.step()
+        o_ours.step()
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adamw_master_weights_bf16(ops):
+    ref = _params(SHAPES)
+    ours = [torch.nn.Parameter(p.detach().to(torch.bfloat16)) for p in ref]
+    for p in ref:
+        p.data = p.data.to(torch.bfloat16).float()
+    o_ref = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    o_ours = ops.FusedAdamW(ours, lr=1e-3, weight_decay=0.01, master_weights=True)
+    for _ in range(4):
+        for a, b in zip(ours, ref):
+            g = torch.randn_like(b).to(torch.bfloat16)
+            a.grad = g.clone()
+            b.grad = g.float()
+        o_ref.step()
+        o_ours.step()
+    for a, b in zip(ours, ref):
+        st = o_ours.state[a]
+        torch.testing.assert_close(st["master"], b.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(a.detach().float(), b.detach().to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("nesterov,dampening", [(False, 0.0), (True, 0.0), (False, 0.1)])
+def test_fused_sgd_matches_torch(ops, nesterov, dampening):
+    ref = _params(SHAPES, seed=3)
+    ours = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    o_ref = torch.optim.SGD(ref, lr=0.05, momentum=0.9, dampening=dampening, weight_decay=1e-3, nesterov=nesterov)
+    o_ours = ops.FusedSGD(ours, lr=0.05, momentum=0.9, dampening=dampening, weight_decay=1e-3, nesterov=nesterov)
+    for _ in range(4):
+        for a, b in zip(ours, ref):
+            g = torch.randn_like(b)
+            a.grad = g.clone()
+            b.grad = g.clone()
+        o_ref.step()
+        o_ours.step()
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_sgd_channels_last_grads(ops):
+    w = torch.nn.Parameter(torch.randn(64, 32, 3, 3, device="cuda").to(memory_format=torch.channels_last))
+    w.grad = torch.randn_like(w)
+    ref = torch.nn.Parameter(w.detach().clone())
+    ref.grad = w.grad.clone()
+    o = ops.FusedSGD([w], lr=0.1, momentum=0.9)
+    r = torch.optim.SGD([ref], lr=0.1, momentum=0.9)
+    o.step()
+    r.step()
+    torch.testing.assert_close(w, ref)
+
+
+def test_fused_clip_and_integrated_clip(ops):
+    ref = _params(SHAPES, seed=5)
+    ours = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    for a, b in zip(ours, ref):
+        a.grad = b.grad.clone()
+    n_ref = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    n_ours = ops.fused_clip_grad_norm_(ours, 1.0)
+    torch.testing.assert_close(n_ours.reshape(()), n_ref, rtol=1e-5, atol=1e-5)
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-6)
+    # integrated: clip inside FusedSGD.step must equal clip-then-step
+    ref2 = _params(SHAPES, seed=6)
+    ours2 = [torch.nn.Parameter(p.detach().clone()) for p in ref2]
+    for a, b in zip(ours2, ref2):
+        a.grad = b.grad.clone()
+    torch.nn.utils.clip_grad_norm_(ref2, 0.5)
+    torch.optim.SGD(ref2, lr=0.1).step()
+    o = ops.FusedSGD(ours2, lr=0.1)
+    o.set_grad_clipping(0.5)
+    o.step()
+    for a, b in zip(ours2, ref2):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_scaler_skips_on_inf_without_sync(ops):
+    ps = _params([(1000,), (33,)])
+    before = [p.detach().clone() for p in ps]
+    opt = ops.FusedAdamW(ps, lr=1e-2)
+    scaler = ops.DeviceGradScaler(init_scale=1024.0, growth_interval=1)
+    loss = torch.zeros((), device="cuda", requires_grad=True)
+    scaler.scale(loss)
+    ps[0].grad[3] = float("inf")
+    scaler.step(opt)
+    scaler.update()
+    for p, b in zip(ps, before):
+        torch.testing.assert_close(p.detach(), b)
+    assert scaler.get_scale() == 512.0
+    assert float(opt._step_tensor(ps[0].device).item()) == 0.0
+    ps[0].grad.zero_()
+    scaler.step(opt)
+    scaler.update()
+    assert float(opt._step_tensor(ps[0].device).item()) == 1.0
+    assert scaler.get_scale() == 1024.0
+
+
+def _ref_ln(x, w, b, eps, rms):
+    xf = x.float()
+    if rms:
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    else:
+        y = torch.nn.functional.layer_norm(xf, (x.shape[-1],), w.float(), b.float() if b is not None else None, eps)
+    return y
+
+
+@pytest.mark.parametrize("H", [64, 768, 1000, 1024, 1600, 4096, 8192])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_fwd_bwd(ops, H, dtype, rms):
+    torch.manual_seed(H)
+    rows = 257
+    x = (torch.randn(rows, H, device="cuda") * 3 + 1).to(dtype).requires_grad_(True)
+    w = (torch.rand(H, device="cuda") + 0.5).to(dtype).requires_grad_(True)
+    b = None if rms else (torch.randn(H, device="cuda") * 0.1).to(dtype).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = None if b is None else b.detach().float().requires_grad_(True)
+    y = ops.rms_norm(x, w, 1e-5) if rms else ops.layer_norm(x, w, b, 1e-5)
+    yr = _ref_ln(xr, wr, br, 1e-5, rms)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    gtol = dict(rtol=3e-2, atol=5e-1) if dtype == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(w.grad.float(), wr.grad, **gtol)
+    if b is not None:
+        torch.testing.assert_close(b.grad.float(), br.grad, **gtol)
+
+
+def test_ddp_single_rank_grads_match(ops):
+    from determined_amd.models.resnet import resnet18
+    from determined_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    m_ref = copy.deepcopy(m)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=1)
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    for it in range(2):
+        ddp.zero_grad()
+        m_ref.zero_grad()
+        ddp(x).sum().backward()
+        ddp.finish()
+        m_ref(x).sum().backward()
+        for (n, p), (_, q) in zip(m.named_parameters(), m_ref.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-4, msg=n)

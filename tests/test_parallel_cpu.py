@@ -1,0 +1,95 @@
+"""Data-parallel engine correctness on CPU with gloo (world_size 2)."""
+
+import copy
+
+import torch
+
+from tests.dist_utils import run_distributed
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(
+        torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8), torch.nn.ReLU(),
+        torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 5),
+    )
+
+
+def _data(rank):
+    g = torch.Generator()
+    g.manual_seed(100 + rank)
+    return torch.randn(4, 3, 8, 8, generator=g)
+
+
+def _ddp_worker(rank, world, bucket_mb, accumulate):
+    from determined_amd.parallel.ddp import DistributedDataParallel
+
+    m = _model().to(memory_format=torch.channels_last)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb)
+    out = []
+    for it in range(3):
+        ddp.zero_grad()
+        if accumulate:
+            with ddp.no_sync():
+                ddp(_data(rank + 10 * it)).sum().backward()
+        ddp(_data(rank + 10 * it + 5)).sum().backward()
+        ddp.finish()
+        out.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    return out
+
+
+def _reference(world, accumulate):
+    m = _model().to(memory_format=torch.channels_last)
+    res = []
+    for it in range(3):
+        grads = None
+        for r in range(world):
+            mm = copy.deepcopy(m)
+            mm.zero_grad()
+            if accumulate:
+                mm(_data(r + 10 * it)).sum().backward()
+            mm(_data(r + 10 * it + 5)).sum().backward()
+            g = {n: p.grad.clone() for n, p in mm.named_parameters()}
+            grads = g if grads is None else {k: grads[k] + g[k] for k in g}
+        res.append({k: v / world for k, v in grads.items()})
+    return res
+
+
+def test_ddp_gloo_matches_averaged_grads():
+    outs = run_distributed(_ddp_worker, world=2, args=(0.0005, False))
+    ref = _reference(2, False)
+    for rank_out in outs:
+        for it in range(3):
+            for k in ref[it]:
+                torch.testing.assert_close(rank_out[it][k], ref[it][k], rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_gloo_no_sync_accumulation():
+    outs = run_distributed(_ddp_worker, world=2, args=(1.0, True))
+    ref = _reference(2, True)
+    for rank_out in outs:
+        for it in range(3):
+            for k in ref[it]:
+                torch.testing.assert_close(rank_out[it][k], ref[it][k], rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_single_process_grad_views():
+    from determined_amd.parallel.ddp import DistributedDataParallel
+
+    m = _model().to(memory_format=torch.channels_last)
+    ref = copy.deepcopy(m)
+    ddp = DistributedDataParallel(m)
+    x = _data(0)
+    ddp(x).sum().backward()
+    ddp.finish()
+    ref(x).sum().backward()
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad)
+        assert p.grad.stride() == p.stride(), n
+    # zero_grad(set_to_none=True) by the user must not break bucket views
+    for p in m.parameters():
+        p.grad = None
+    ddp(x).sum().backward()
+    ddp.finish()
+    ptrs = {b.buffer.data_ptr() for b in ddp._buckets}
+    assert all(any(p.grad.data_ptr() >= bp for bp in ptrs) for p in m.parameters())
