@@ -38,6 +38,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--conv-benchmark", type=int, default=0,
+                   help="1: let MIOpen search for the fastest conv solvers (torch.backends.cudnn.benchmark)")
     return p.parse_args()
 
 
@@ -48,6 +50,7 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(local)
+    torch.backends.cudnn.benchmark = bool(a.conv_benchmark)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 

@@ -48,6 +48,15 @@ int damd_norm_bwd_blocks(int64_t);
 void damd_norm_bwd_launch(const void*, const void*, const float*, const float*, const void*, void*, float*,
                           float*, int64_t, int, int, int, int, hipStream_t);
 void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
+// launchers (bn.hip)
+int damd_bn_num_blocks(int64_t, int);
+void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
+                        float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t);
+void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
+                               hipStream_t);
+void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
+                        const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
+                        hipStream_t);
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -246,9 +255,117 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, cons
   return {dx, dgamma, dbeta};
 }
 
+// ----------------------------------------------------------------------------- BatchNorm(+add)+ReLU, NHWC
+bool nhwc_dense(const at::Tensor& t) {
+  if (t.dim() == 4) return t.is_contiguous(at::MemoryFormat::ChannelsLast);
+  return t.is_contiguous();
+}
+
+void check_bn_tensor(const at::Tensor& t, const at::Tensor& ref, const char* what) {
+  TORCH_CHECK(t.is_cuda(), what, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == ref.scalar_type(), what, " dtype must match x");
+  TORCH_CHECK(t.sizes() == ref.sizes(), what, " shape must match x");
+  TORCH_CHECK(nhwc_dense(t), what, " must be channels-last dense");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+}
+
+int64_t bn_channels(const at::Tensor& x) { return x.dim() == 4 ? x.size(1) : x.size(-1); }
+
+bool bn_supported(const at::Tensor& x) {
+  const int64_t C = bn_channels(x);
+  const int64_t tpr = C / 8;
+  return x.is_cuda() && (C % 8) == 0 && tpr > 0 && (tpr & (tpr - 1)) == 0 && nhwc_dense(x) &&
+         (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+         (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
+}
+
+std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
+                                   const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                                   const c10::optional<at::Tensor>& residual, bool relu) {
+  TORCH_CHECK(bn_supported(x), "bn_act_fwd: unsupported input layout/shape");
+  const int64_t C = bn_channels(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C && weight.scalar_type() == bias.scalar_type(),
+              "weight/bias must have C elements and one dtype");
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_bn_tensor(*residual, x, "residual");
+    rp = residual->data_ptr();
+  }
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    TORCH_CHECK(running_mean->scalar_type() == at::kFloat && running_var->scalar_type() == at::kFloat,
+                "running stats must be float32");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  auto fopts = x.options().dtype(at::kFloat);
+  const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
+  auto part = at::empty({nb, 2, C}, fopts);
+  auto stats = at::empty({4, C}, fopts);  // mean, invstd, scale, shift
+  auto y = at::empty_like(x);
+  damd_bn_fwd_launch(x.data_ptr(), rp, y.data_ptr(), M, static_cast<int>(C), weight.data_ptr(), bias.data_ptr(), rm, rv,
+                     static_cast<float>(momentum), static_cast<float>(eps), part.data_ptr<float>(),
+                     stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
+                     stats[3].data_ptr<float>(), relu, dtype_code(x), dtype_code(weight), cur_stream());
+  return {y, stats};
+}
+
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& residual, bool relu) {
+  TORCH_CHECK(bn_supported(x), "bn_apply: unsupported input layout/shape");
+  const int64_t C = bn_channels(x);
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_bn_tensor(*residual, x, "residual");
+    rp = residual->data_ptr();
+  }
+  auto y = at::empty_like(x);
+  auto sc = scale.to(at::kFloat).contiguous();
+  auto sh = shift.to(at::kFloat).contiguous();
+  damd_bn_apply_only_launch(x.data_ptr(), rp, y.data_ptr(), x.numel() / C, static_cast<int>(C), sc.data_ptr<float>(),
+                            sh.data_ptr<float>(), relu, dtype_code(x), cur_stream());
+  return y;
+}
+
+std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
+                                   const c10::optional<at::Tensor>& residual, const at::Tensor& stats,
+                                   const at::Tensor& weight, bool relu, bool need_dres) {
+  check_bn_tensor(dy, x, "dy");
+  const int64_t C = bn_channels(x);
+  const int64_t M = x.numel() / C;
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_bn_tensor(*residual, x, "residual");
+    rp = residual->data_ptr();
+  }
+  auto fopts = x.options().dtype(at::kFloat);
+  const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
+  auto part = at::empty({nb, 2, C}, fopts);
+  auto coef = at::empty({3, C}, fopts);
+  auto dgamma = at::empty({C}, weight.options());
+  auto dbeta = at::empty({C}, weight.options());
+  auto dx = at::empty_like(x);
+  // dres == dy' (masked dy).  Without ReLU it is dy itself: no kernel write needed.
+  const bool write_dres = need_dres && relu;
+  at::Tensor dres = write_dres ? at::empty_like(x) : (need_dres ? dy : at::Tensor());
+  damd_bn_bwd_launch(dy.data_ptr(), x.data_ptr(), rp, M, static_cast<int>(C), stats[0].data_ptr<float>(),
+                     stats[1].data_ptr<float>(), stats[2].data_ptr<float>(), stats[3].data_ptr<float>(),
+                     part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(),
+                     dx.data_ptr(), write_dres ? dres.data_ptr() : nullptr, relu, dtype_code(x), dtype_code(weight),
+                     cur_stream());
+  return {dx, dgamma, dbeta, dres};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("bn_supported", &bn_supported);
+  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("bn_apply", &bn_apply);
   m.doc() = "determined_amd CDNA4 HIP kernels";
   m.def("build_chunk_table", &build_chunk_table);
   m.def("chunk_entry_bytes", &chunk_entry_bytes);

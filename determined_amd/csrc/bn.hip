@@ -1,0 +1,494 @@
+// Channels-last (NHWC) BatchNorm + optional residual add + optional ReLU, fwd and bwd, for gfx950.
+//
+// ResNet training is bandwidth-bound on BN/ReLU/add, not on its convolutions: stock PyTorch
+// runs BN stats, BN transform, residual add, ReLU, ReLU-bwd, BN-bwd-reduce and BN-bwd-elementwise
+// as seven HBM passes.  Here one "BNAct" op is four passes total:
+//   fwd:  stats (read x)  ->  apply  y = relu(x*scale + shift [+ res])   (read x[,res], write y)
+//   bwd:  reduce (read dy, x[,res]) -> dx = A*dy' + B*x + C, dres = dy'  (read dy, x[,res]; write)
+// where dy' = dy * [pre-activation > 0].  The ReLU mask is RECOMPUTED from x (and res) instead
+// of reading the saved output, so the backward never touches y.
+//
+// Tensor view: x is [M, C] row-major (M = N*H*W).  A thread owns one 16-byte vector of
+// 8 channels (bf16) and walks rows; with TPR = C/8 threads per row a 256-thread block
+// covers 256/TPR rows per iteration, so every wave-instruction reads 1 KiB contiguous.
+// Statistics use a per-channel shift K_c = x[0, c] ("shifted data" variance): sums of
+// (x-K) and (x-K)^2 are plain sums, so block partials merge by addition with no
+// E[x^2]-E[x]^2 cancellation when |mean| >> std.
+// Requirements (checked on the host, torch fallback otherwise): C % 8 == 0 and C/8 a power
+// of two (every ResNet width) and 16-byte aligned base pointers.
+
+#include "common.h"
+
+namespace damd {
+
+constexpr int kBNThreads = 256;
+
+template <typename T> struct V8;
+template <> struct V8<bf16_t> {
+  static __device__ __forceinline__ void ld(const bf16_t* p, float* o) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = bf2f(r.v[k]);
+  }
+  static __device__ __forceinline__ void st(bf16_t* p, const float* o) {
+    bf16x8 r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = f2bf(o[k]);
+    *reinterpret_cast<bf16x8*>(p) = r;
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void ld(const float* p, float* o) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float* o) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+};
+
+struct Geo {
+  int TPR;   // threads (8-channel vectors) per row
+  int RS;    // rows per block iteration (>=1)
+  int G;     // channel groups per thread (TPR > 256)
+};
+
+__device__ __forceinline__ Geo geo(int C) {
+  Geo g;
+  g.TPR = C / 8;
+  g.RS = g.TPR <= kBNThreads ? kBNThreads / g.TPR : 1;
+  g.G = g.TPR <= kBNThreads ? 1 : g.TPR / kBNThreads;
+  return g;
+}
+
+// ----------------------------------------------------------------------------- fwd stats
+// part: [nb][2][C]  (sum(x-K), sum((x-K)^2)) per block.
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
+  const Geo g = geo(C);
+  const int tid = threadIdx.x;
+  const int cg0 = g.TPR <= kBNThreads ? tid % g.TPR : tid;
+  const int rsub = g.TPR <= kBNThreads ? tid / g.TPR : 0;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  __shared__ float red[kBNThreads * 8];
+  for (int gi = 0; gi < g.G; ++gi) {
+    const int cg = cg0 + gi * kBNThreads;
+    float K[8], s[8], ss[8];
+    V8<T>::ld(x + cg * 8, K);  // row 0 pilot values
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; ss[k] = 0.f; }
+    int64_t r = r0 + rsub;
+    for (; r + 3 * g.RS < r1; r += 4 * g.RS) {
+      float a[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) V8<T>::ld(x + (r + u * g.RS) * C + cg * 8, a[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { const float d = a[u][k] - K[k]; s[k] += d; ss[k] += d * d; }
+    }
+    for (; r < r1; r += g.RS) {
+      float a[8];
+      V8<T>::ld(x + r * C + cg * 8, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { const float d = a[k] - K[k]; s[k] += d; ss[k] += d * d; }
+    }
+    // merge the RS row-lanes that share a channel group (plain sums)
+    for (int which = 0; which < 2; ++which) {
+      float* v = which == 0 ? s : ss;
+      if (g.RS > 1) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[tid * 8 + k] = v[k];
+        __syncthreads();
+        if (rsub == 0) {
+          for (int q = 1; q < g.RS; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += red[(q * g.TPR + cg0) * 8 + k];
+        }
+      }
+      if (rsub == 0) {
+        float* dst = part + (static_cast<int64_t>(blockIdx.x) * 2 + which) * C + cg * 8;
+        V8<float>::st(dst, v);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- partial reduction
+// Sums part[nb][2][C] over nb for 64 channels per block.  1024 threads = 64 channels x 16
+// lanes; each lane keeps 8 independent accumulators so its loads are issued back to back
+// (a serial per-thread chain over ~1000 partial rows costs ~70 us in L2 round trips).
+// Result (deterministic order) lands in thread lane==0's (s, ss).
+constexpr int kFinThreads = 1024;
+constexpr int kFinLanes = kFinThreads / 64;
+
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int nb, int C, int c, int q,
+                                                float& s, float& ss) {
+  __shared__ float rs[kFinLanes][64], rq[kFinLanes][64];
+  float a0[8], a1[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { a0[u] = 0.f; a1[u] = 0.f; }
+  if (c < C) {
+    int bi = q;
+    for (; bi + 7 * kFinLanes < nb; bi += 8 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t row = static_cast<int64_t>(bi + u * kFinLanes) * 2;
+        a0[u] += part[row * C + c];
+        a1[u] += part[(row + 1) * C + c];
+      }
+    }
+    for (; bi < nb; bi += kFinLanes) {
+      a0[0] += part[(static_cast<int64_t>(bi) * 2) * C + c];
+      a1[0] += part[(static_cast<int64_t>(bi) * 2 + 1) * C + c];
+    }
+  }
+  float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { t0 += a0[u]; t1 += a1[u]; }
+  const int lane = threadIdx.x & 63;
+  rs[q][lane] = t0;
+  rq[q][lane] = t1;
+  __syncthreads();
+  s = 0.f;
+  ss = 0.f;
+  if (q == 0) {
+#pragma unroll
+    for (int k = 0; k < kFinLanes; ++k) { s += rs[k][lane]; ss += rq[k][lane]; }
+  }
+}
+
+// ----------------------------------------------------------------------------- fwd finalize
+// Produces mean/invstd (saved for bwd), folded scale/shift (for apply) and updates the
+// running statistics.  grid = ceil(C/64) blocks of 1024 threads.
+template <typename WT>
+__global__ void __launch_bounds__(kFinThreads)
+bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, int64_t rows_per_block,
+                   const void* __restrict__ xbase, int x_is_bf16, float momentum, float eps,
+                   const WT* __restrict__ w, const WT* __restrict__ b, float* __restrict__ run_mean,
+                   float* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s, ss;
+  reduce_partials(part, nb, C, c, q, s, ss);
+  if (q == 0 && c < C) {
+    const float K = x_is_bf16 ? bf2f(static_cast<const bf16_t*>(xbase)[c]) : static_cast<const float*>(xbase)[c];
+    const float n = static_cast<float>(M);
+    const float dm = s / n;
+    const float var = fmaxf(ss / n - dm * dm, 0.f);
+    const float mean = K + dm;
+    const float invstd = rsqrtf(var + eps);
+    mean_out[c] = mean;
+    invstd_out[c] = invstd;
+    const float wv = w ? Elem<WT>::ld(w, c) : 1.f;
+    const float bv = b ? Elem<WT>::ld(b, c) : 0.f;
+    scale_out[c] = wv * invstd;
+    shift_out[c] = bv - mean * wv * invstd;
+    if (run_mean) {
+      const float unbiased = M > 1 ? var * n / (n - 1.f) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- fwd apply
+template <typename T, bool RES, bool RELU>
+__global__ void __launch_bounds__(kBNThreads)
+bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+                const T* __restrict__ res, T* __restrict__ y, int64_t V, int TPR) {
+  const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;  // multiple of TPR
+  const int cg = static_cast<int>(T0 % TPR);
+  float sc[8], sh[8];
+  V8<float>::ld(scale + cg * 8, sc);
+  V8<float>::ld(shift + cg * 8, sh);
+  for (int64_t v = T0; v < V; v += stride) {
+    float a[8], r[8];
+    V8<T>::ld(x + v * 8, a);
+    if (RES) V8<T>::ld(res + v * 8, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = a[k] * sc[k] + sh[k];
+      if (RES) o += r[k];
+      if (RELU) o = fmaxf(o, 0.f);
+      a[k] = o;
+    }
+    V8<T>::st(y + v * 8, a);
+  }
+}
+
+// ----------------------------------------------------------------------------- bwd reduce
+// part: [nb][2][C] = (sum dy', sum dy' * (x - mean))
+template <typename T, bool RES, bool RELU>
+__global__ void __launch_bounds__(kBNThreads)
+bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
+                     const float* __restrict__ mean, const float* __restrict__ scale,
+                     const float* __restrict__ shift, int64_t M, int C, int64_t rows_per_block,
+                     float* __restrict__ part) {
+  const Geo g = geo(C);
+  const int tid = threadIdx.x;
+  const int cg0 = g.TPR <= kBNThreads ? tid % g.TPR : tid;
+  const int rsub = g.TPR <= kBNThreads ? tid / g.TPR : 0;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  __shared__ float red[kBNThreads * 8];
+  for (int gi = 0; gi < g.G; ++gi) {
+    const int cg = cg0 + gi * kBNThreads;
+    float mu[8], sc[8], sh[8], s[8], sx[8];
+    V8<float>::ld(mean + cg * 8, mu);
+    if (RELU) { V8<float>::ld(scale + cg * 8, sc); V8<float>::ld(shift + cg * 8, sh); }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; sx[k] = 0.f; }
+    int64_t r = r0 + rsub;
+    for (; r + g.RS < r1; r += 2 * g.RS) {
+      float d[2][8], a[2][8], rr[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t off = (r + u * g.RS) * C + cg * 8;
+        V8<T>::ld(dy + off, d[u]);
+        V8<T>::ld(x + off, a[u]);
+        if (RES && RELU) V8<T>::ld(res + off, rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float dv = d[u][k];
+          if (RELU) {
+            float z = a[u][k] * sc[k] + sh[k];
+            if (RES) z += rr[u][k];
+            dv = z > 0.f ? dv : 0.f;
+          }
+          s[k] += dv;
+          sx[k] += dv * (a[u][k] - mu[k]);
+        }
+    }
+    for (; r < r1; r += g.RS) {
+      float d[8], a[8], rr[8];
+      const int64_t off = r * C + cg * 8;
+      V8<T>::ld(dy + off, d);
+      V8<T>::ld(x + off, a);
+      if (RES && RELU) V8<T>::ld(res + off, rr);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float dv = d[k];
+        if (RELU) {
+          float z = a[k] * sc[k] + sh[k];
+          if (RES) z += rr[k];
+          dv = z > 0.f ? dv : 0.f;
+        }
+        s[k] += dv;
+        sx[k] += dv * (a[k] - mu[k]);
+      }
+    }
+    for (int which = 0; which < 2; ++which) {
+      float* v = which == 0 ? s : sx;
+      if (g.RS > 1) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[tid * 8 + k] = v[k];
+        __syncthreads();
+        if (rsub == 0) {
+          for (int q = 1; q < g.RS; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += red[(q * g.TPR + cg0) * 8 + k];
+        }
+      }
+      if (rsub == 0) V8<float>::st(part + (static_cast<int64_t>(blockIdx.x) * 2 + which) * C + cg * 8, v);
+    }
+  }
+}
+
+// bwd finalize: dgamma, dbeta (fp32) and the elementwise coefficients A, B, Cc:
+//   dx = A*dy' + B*x + Cc
+// dgamma/dbeta are written directly in the parameter dtype (no separate cast kernels).
+template <typename WT>
+__global__ void __launch_bounds__(kFinThreads)
+bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
+                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                       const float* __restrict__ scale, WT* __restrict__ dgamma, WT* __restrict__ dbeta,
+                       float* __restrict__ coef /* [3][C] */) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s, sx;
+  reduce_partials(part, nb, C, c, q, s, sx);
+  if (q == 0 && c < C) {
+    const float is = invstd[c];
+    const float dg = sx * is;  // sum dy' * xhat
+    Elem<WT>::st(dgamma, c, dg);
+    Elem<WT>::st(dbeta, c, s);
+    const float n = static_cast<float>(M);
+    const float sc = scale[c];
+    const float A = sc;
+    const float B = -sc * is * dg / n;
+    const float Cc = -sc * s / n - B * mean[c];
+    coef[c] = A;
+    coef[C + c] = B;
+    coef[2 * C + c] = Cc;
+  }
+}
+
+template <typename T, bool RES, bool RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(kBNThreads)
+bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
+                    const float* __restrict__ scale, const float* __restrict__ shift,
+                    const float* __restrict__ coef, int C, T* __restrict__ dx, T* __restrict__ dres, int64_t V,
+                    int TPR) {
+  const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
+  const int cg = static_cast<int>(T0 % TPR);
+  float A[8], B[8], Cc[8], sc[8], sh[8];
+  V8<float>::ld(coef + cg * 8, A);
+  V8<float>::ld(coef + C + cg * 8, B);
+  V8<float>::ld(coef + 2 * C + cg * 8, Cc);
+  if (RELU) { V8<float>::ld(scale + cg * 8, sc); V8<float>::ld(shift + cg * 8, sh); }
+  for (int64_t v = T0; v < V; v += stride) {
+    float d[8], a[8], rr[8], o[8];
+    V8<T>::ld(dy + v * 8, d);
+    V8<T>::ld(x + v * 8, a);
+    if (RES && RELU) V8<T>::ld(res + v * 8, rr);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float dv = d[k];
+      if (RELU) {
+        float z = a[k] * sc[k] + sh[k];
+        if (RES) z += rr[k];
+        dv = z > 0.f ? dv : 0.f;
+      }
+      d[k] = dv;
+      o[k] = A[k] * dv + B[k] * a[k] + Cc[k];
+    }
+    V8<T>::st(dx + v * 8, o);
+    if (WRITE_DRES) V8<T>::st(dres + v * 8, d);
+  }
+}
+
+}  // namespace damd
+
+using namespace damd;
+
+namespace {
+int64_t rows_per_block_for(int64_t M, int C, int* nb_out) {
+  // ~1024 blocks (4 per CU) for big tensors; at least 16 rows per block.
+  int64_t nb = 1024;
+  int64_t rpb = (M + nb - 1) / nb;
+  const int RS = (C / 8) <= kBNThreads ? kBNThreads / (C / 8) : 1;
+  if (rpb < 4 * RS) rpb = 4 * RS;
+  nb = (M + rpb - 1) / rpb;
+  *nb_out = static_cast<int>(nb);
+  return rpb;
+}
+
+int apply_grid(int64_t V, int TPR) {
+  // grid*256 must be a multiple of TPR (channel group constant per thread)
+  int64_t blocks = (V + kBNThreads - 1) / kBNThreads;
+  if (blocks > 2048) blocks = 2048;
+  const int mult = TPR > kBNThreads ? TPR / kBNThreads : 1;
+  blocks = (blocks + mult - 1) / mult * mult;
+  return static_cast<int>(blocks);
+}
+}  // namespace
+
+int damd_bn_num_blocks(int64_t M, int C) {
+  int nb;
+  rows_per_block_for(M, C, &nb);
+  return nb;
+}
+
+// x_dtype/w_dtype: 0 = fp32, 1 = bf16
+void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int C, const void* w, const void* b,
+                        float* run_mean, float* run_var, float momentum, float eps, float* part, float* mean,
+                        float* invstd, float* scale, float* shift, int relu, int x_dtype, int w_dtype,
+                        hipStream_t st) {
+  int nb;
+  const int64_t rpb = rows_per_block_for(M, C, &nb);
+  if (x_dtype == 1)
+    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+  const dim3 fg((C + 63) / 64);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+                       static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+                       static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
+  const int TPR = C / 8;
+  const int64_t V = M * C / 8;
+  const dim3 ag(apply_grid(V, TPR));
+#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR)
+  if (x_dtype == 1) {
+    if (res) { if (relu) APPLY(bf16_t, true, true); else APPLY(bf16_t, true, false); }
+    else { if (relu) APPLY(bf16_t, false, true); else APPLY(bf16_t, false, false); }
+  } else {
+    if (res) { if (relu) APPLY(float, true, true); else APPLY(float, true, false); }
+    else { if (relu) APPLY(float, false, true); else APPLY(float, false, false); }
+  }
+#undef APPLY
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_bn_apply_only_launch(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
+                               const float* shift, int relu, int x_dtype, hipStream_t st) {
+  const int TPR = C / 8;
+  const int64_t V = M * C / 8;
+  const dim3 ag(apply_grid(V, TPR));
+#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR)
+  if (x_dtype == 1) {
+    if (res) { if (relu) APPLY(bf16_t, true, true); else APPLY(bf16_t, true, false); }
+    else { if (relu) APPLY(bf16_t, false, true); else APPLY(bf16_t, false, false); }
+  } else {
+    if (res) { if (relu) APPLY(float, true, true); else APPLY(float, true, false); }
+    else { if (relu) APPLY(float, false, true); else APPLY(float, false, false); }
+  }
+#undef APPLY
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t M, int C, const float* mean,
+                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
+                        void* dgamma, void* dbeta, void* dx, void* dres, int relu, int x_dtype, int w_dtype,
+                        hipStream_t st) {
+  int nb;
+  const int64_t rpb = rows_per_block_for(M, C, &nb);
+  const bool has_res = res != nullptr;
+#define RED(T, R, A) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part)
+  if (x_dtype == 1) {
+    if (has_res) { if (relu) RED(bf16_t, true, true); else RED(bf16_t, true, false); }
+    else { if (relu) RED(bf16_t, false, true); else RED(bf16_t, false, false); }
+  } else {
+    if (has_res) { if (relu) RED(float, true, true); else RED(float, true, false); }
+    else { if (relu) RED(float, false, true); else RED(float, false, false); }
+  }
+#undef RED
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
+  const int TPR = C / 8;
+  const int64_t V = M * C / 8;
+  const dim3 ag(apply_grid(V, TPR));
+  const bool wd = dres != nullptr;
+#define BAP(T, R, A, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR)
+  if (x_dtype == 1) {
+    if (has_res) { if (relu) { if (wd) BAP(bf16_t, true, true, true); else BAP(bf16_t, true, true, false); }
+                   else { if (wd) BAP(bf16_t, true, false, true); else BAP(bf16_t, true, false, false); } }
+    else { if (relu) { if (wd) BAP(bf16_t, false, true, true); else BAP(bf16_t, false, true, false); }
+           else { if (wd) BAP(bf16_t, false, false, true); else BAP(bf16_t, false, false, false); } }
+  } else {
+    if (has_res) { if (relu) { if (wd) BAP(float, true, true, true); else BAP(float, true, true, false); }
+                   else { if (wd) BAP(float, true, false, true); else BAP(float, true, false, false); } }
+    else { if (relu) { if (wd) BAP(float, false, true, true); else BAP(float, false, true, false); }
+           else { if (wd) BAP(float, false, false, true); else BAP(float, false, false, false); } }
+  }
+#undef BAP
+  DAMD_CHECK_LAUNCH();
+}

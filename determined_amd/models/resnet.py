@@ -12,6 +12,8 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
+from determined_amd.ops.bn import BatchNormAct2d
+
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -28,20 +30,18 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * self.expansion
         self.conv1 = conv1x1(cin, width)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormAct2d(width)
         self.conv2 = conv3x3(width, width, stride)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNormAct2d(width)
         self.conv3 = conv1x1(width, cout)
-        self.bn3 = nn.BatchNorm2d(cout)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BatchNormAct2d(cout)  # fused: relu(bn3(conv3) + identity)
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + identity)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
 
 
 class BasicBlock(nn.Module):
@@ -50,17 +50,15 @@ class BasicBlock(nn.Module):
     def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None) -> None:
         super().__init__()
         self.conv1 = conv3x3(cin, width, stride)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormAct2d(width)
         self.conv2 = conv3x3(width, width)
-        self.bn2 = nn.BatchNorm2d(width)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn2 = BatchNormAct2d(width)
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), identity)
 
 
 class ResNet(nn.Module):
@@ -69,8 +67,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct2d(64)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
@@ -81,7 +78,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -96,7 +93,7 @@ class ResNet(nn.Module):
         if stride != 1 or self.inplanes != width * block.expansion:
             downsample = nn.Sequential(
                 conv1x1(self.inplanes, width * block.expansion, stride),
-                nn.BatchNorm2d(width * block.expansion),
+                BatchNormAct2d(width * block.expansion, act=False),
             )
         mods = [block(self.inplanes, width, stride, downsample)]
         self.inplanes = width * block.expansion
@@ -104,7 +101,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -58,6 +58,7 @@ from determined_amd.ops.norm import (  # noqa: E402
     rms_norm,
 )
 from determined_amd.ops.scaler import DeviceGradScaler  # noqa: E402
+from determined_amd.ops.bn import BatchNormAct2d  # noqa: E402
 
 __all__ = [
     "available",
@@ -70,4 +71,5 @@ __all__ = [
     "layer_norm",
     "rms_norm",
     "DeviceGradScaler",
+    "BatchNormAct2d",
 ]

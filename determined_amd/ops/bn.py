@@ -1,0 +1,94 @@
+"""Fused channels-last BatchNorm (+ residual add) (+ ReLU) backed by csrc/bn.hip.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and
+state-dict keys) whose forward takes an optional residual and applies ReLU in the same pass:
+``y = relu(bn(x) + residual)``.  Training on a supported GPU tensor runs 2 kernels forward
+(stats, apply) and 2 backward (reduce, apply) instead of stock PyTorch's 7 HBM passes.
+CPU tensors / unsupported shapes use the exact PyTorch composition.
+"""
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+        from determined_amd import ops
+
+        y, stats = ops.ext().bn_act_fwd(x, weight, bias, running_mean, running_var, float(momentum),
+                                        float(eps), residual, bool(relu))
+        ctx.save_for_backward(x, residual if residual is not None else None, stats, weight)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from determined_amd import ops
+
+        x, residual, stats, weight = ctx.saved_tensors
+        mf = torch.channels_last if x.dim() == 4 else torch.contiguous_format
+        dy = dy.contiguous(memory_format=mf)
+        dx, dg, db, dres = ops.ext().bn_act_bwd(dy, x, residual, stats, weight, bool(ctx.relu), bool(ctx.has_res))
+        return (dx, dg, db, None, None,
+                dres if ctx.has_res else None, None, None, None)
+
+
+def _torch_bn_act(bn: nn.BatchNorm2d, x, residual, relu, momentum):
+    y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                     bn.training or not bn.track_running_stats, momentum, bn.eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``relu(BatchNorm2d(x) [+ residual])`` with the fused HIP kernels on channels-last input."""
+
+    def __init__(self, num_features: int, act: bool = True, eps: float = 1e-5, momentum: Optional[float] = 0.1,
+                 **kw) -> None:
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.act = act
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:
+                momentum = 1.0 / float(self.num_batches_tracked)
+        if not x.is_cuda or not self.affine:
+            return _torch_bn_act(self, x, residual, self.act, momentum)
+        from determined_amd import ops
+
+        e = ops.ext()
+        if not e.bn_supported(x) or (residual is not None and residual.stride() != x.stride()):
+            return _torch_bn_act(self, x, residual, self.act, momentum)
+        if self.training or not self.track_running_stats:
+            rm = self.running_mean if self.track_running_stats else None
+            rv = self.running_var if self.track_running_stats else None
+            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act)
+        # eval: fold running statistics; one elementwise pass.
+        scale = self.weight.float() * torch.rsqrt(self.running_var + self.eps)
+        shift = self.bias.float() - self.running_mean * scale
+        if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
+            y = x * scale.view(1, -1, 1, 1).to(x.dtype) + shift.view(1, -1, 1, 1).to(x.dtype)
+            if residual is not None:
+                y = y + residual
+            return F.relu(y) if self.act else y
+        return e.bn_apply(x, scale, shift, residual, self.act)
+
+    def _apply(self, fn, recurse: bool = True):
+        # Running statistics always stay fp32 (a bf16 running_var loses the update signal).
+        super()._apply(fn, recurse)
+        for name in ("running_mean", "running_var"):
+            b = getattr(self, name, None)
+            if b is not None and b.is_floating_point() and b.dtype != torch.float32:
+                self._buffers[name] = b.float()
+        return self
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", act={self.act}"

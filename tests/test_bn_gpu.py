@@ -1,0 +1,97 @@
+"""Fused NHWC BatchNorm(+add)(+ReLU) kernels vs an fp32 PyTorch reference (MI355X)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bnmod():
+    import determined_amd.ops as ops
+
+    ops.ext()
+    return ops
+
+
+def _ref(x, w, b, rm, rv, res, relu, mom, eps):
+    y = F.batch_norm(x, rm, rv, w, b, True, mom, eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14), (2, 256, 7, 9), (3, 2048, 3, 3), (5, 8, 6, 6), (2, 4096, 2, 2)])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_act_train(bnmod, shape, res, relu, dtype):
+    torch.manual_seed(sum(shape))
+    N, C, H, W = shape
+    m = bnmod.BatchNormAct2d(C, act=relu).cuda()
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    m = m.to(dtype)
+    x = (torch.randn(shape, device="cuda") * 2 + 3).to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    r = None
+    if res:
+        r = torch.randn(shape, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+        r.requires_grad_(True)
+    y = m(x, r)
+    # fp32 reference
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if res else None
+    wr = m.weight.detach().float().requires_grad_(True)
+    br = m.bias.detach().float().requires_grad_(True)
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    yr = _ref(xr, wr, br, rm, rv, rr, relu, 0.1, 1e-5)
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(m.running_mean, rm, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(m.running_var, rv, rtol=1e-3, atol=1e-3)
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    gtol = dict(rtol=3e-2, atol=3e-1) if dtype == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, **gtol)
+    torch.testing.assert_close(m.bias.grad.float(), br.grad, **gtol)
+    if res:
+        torch.testing.assert_close(r.grad.float(), rr.grad, **tol)
+
+
+def test_bn_large_mean_stats_stable(bnmod):
+    # |mean| >> std: shifted-sum statistics must not cancel.
+    C = 64
+    m = bnmod.BatchNormAct2d(C, act=False).cuda()
+    x = (torch.randn(8, C, 32, 32, device="cuda") * 0.01 + 100.0).contiguous(memory_format=torch.channels_last)
+    y = m(x)
+    # float64 CPU reference (a single-pass fp32 E[x^2]-E[x]^2 reference would itself cancel here)
+    xd = x.detach().double().cpu()
+    yr = F.batch_norm(xd, None, None, m.weight.double().cpu(), m.bias.double().cpu(), True, 0.1, 1e-5)
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-3, atol=5e-3)
+
+
+def test_bn_eval_matches(bnmod):
+    C = 256
+    m = bnmod.BatchNormAct2d(C).cuda()
+    with torch.no_grad():
+        m.running_mean.uniform_(-1, 1)
+        m.running_var.uniform_(0.5, 2)
+        m.weight.uniform_(0.5, 1.5)
+    m.eval()
+    x = torch.randn(2, C, 5, 5, device="cuda").contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x)
+    with torch.no_grad():
+        y = m(x, r)
+    yr = F.relu(F.batch_norm(x, m.running_mean, m.running_var, m.weight, m.bias, False, 0.1, 1e-5) + r)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+
+
+def test_bf16_model_keeps_fp32_running_stats(bnmod):
+    m = bnmod.BatchNormAct2d(64).cuda().to(torch.bfloat16)
+    assert m.running_mean.dtype == torch.float32 and m.weight.dtype == torch.bfloat16
