@@ -38,7 +38,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--profile-steps", type=int, default=0)
-    p.add_argument("--conv-benchmark", type=int, default=0,
+    p.add_argument("--conv-benchmark", type=int, default=1,
                    help="1: let MIOpen search for the fastest conv solvers (torch.backends.cudnn.benchmark)")
     return p.parse_args()
 

@@ -1,0 +1,89 @@
+// Native resource scheduler for a resource pool of agents and their slots.
+//
+// Counterpart of the reference's agent resource manager schedulers
+// (master/internal/rm/agentrm/{priority,fair_share,round_robin,fitting,fitting_methods}.go).
+// An MI355X node is one agent with 8 slots (one per GPU, 288 GB HBM each); the scheduler packs
+// concurrent 1-slot trials onto free GPUs or gang-schedules an N-slot distributed trial, and
+// decides which running allocations to preempt.  Pure state machine: the master calls
+// schedule() after every change and acts on the returned decisions.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace damd_native {
+
+enum class Policy { Priority = 0, FairShare = 1, RoundRobin = 2 };
+enum class Fit { Best = 0, Worst = 1 };
+
+struct AgentState {
+  std::string id;
+  int num_slots = 0;
+  std::vector<std::string> slot_owner;  // allocation id or "" per slot
+  int zero_slot_containers = 0;
+  bool enabled = true;
+  int empty() const;
+  int used() const { return num_slots - empty(); }
+};
+
+struct Request {
+  std::string alloc_id;
+  std::string job_id;
+  int slots = 1;
+  int priority = 42;      // smaller value = more important (reference: 1..99, default 42)
+  double weight = 1.0;    // fair share weight
+  int64_t order = 0;      // submission order (queue position)
+  bool preemptible = true;
+  bool allocated = false;
+  bool preempting = false;  // release already requested
+  // agent id -> slot indices
+  std::vector<std::pair<std::string, std::vector<int>>> assignment;
+};
+
+struct Decision {
+  std::vector<std::string> allocated;  // alloc ids newly allocated this round
+  std::vector<std::string> preempt;    // alloc ids that must release their resources
+};
+
+class Scheduler {
+ public:
+  Scheduler(Policy policy, Fit fit, bool preemption) : policy_(policy), fit_(fit), preemption_(preemption) {}
+
+  void add_agent(const std::string& id, int slots);
+  void remove_agent(const std::string& id);  // allocations on it become unallocated (returned lost)
+  void set_agent_enabled(const std::string& id, bool enabled);
+  void add_request(const Request& r);
+  void remove_request(const std::string& alloc_id);  // frees its slots
+  void set_priority(const std::string& job_id, int priority);
+  void set_weight(const std::string& job_id, double weight);
+
+  Decision schedule();
+
+  const std::map<std::string, Request>& requests() const { return reqs_; }
+  const std::map<std::string, AgentState>& agents() const { return agents_; }
+  int total_slots() const;
+  int used_slots() const;
+
+ private:
+  struct Fitting {
+    std::vector<std::pair<std::string, std::vector<int>>> assignment;
+  };
+  bool find_fit(const Request& r, const std::map<std::string, AgentState>& agents, Fitting* out) const;
+  void apply(std::map<std::string, AgentState>& agents, const std::string& alloc_id, const Fitting& f) const;
+  void release(std::map<std::string, AgentState>& agents, const Request& r) const;
+  double score(const Request& r, const AgentState& a) const;
+
+  Decision schedule_priority();
+  Decision schedule_fair_share();
+  Decision schedule_round_robin();
+
+  Policy policy_;
+  Fit fit_;
+  bool preemption_;
+  std::map<std::string, AgentState> agents_;
+  std::map<std::string, Request> reqs_;
+};
+
+}  // namespace damd_native

@@ -1,0 +1,219 @@
+"""The agent: exposes a node's slots to the master and runs tasks on them
+(reference: ``agent/`` in Go, which launches Docker containers).
+
+On an MI355X node the agent owns 8 GPU slots (one per GPU, discovered from the KFD topology in
+sysfs -- the agent never initialises HIP itself, so spawning task processes is safe).  Tasks
+run as process groups with ``HIP_VISIBLE_DEVICES`` set to their slots; stdout/stderr are
+shipped to the master line by line; exit codes are reported back.
+"""
+
+import base64
+import io
+import json
+import logging
+import os
+import pathlib
+import shlex
+import signal
+import socket
+import subprocess
+import sys
+import tarfile
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+from determined_amd.common.api import Session
+
+logger = logging.getLogger("determined_amd.agent")
+
+
+def detect_gpus() -> List[int]:
+    """GPU ordinals from /sys/class/kfd (nodes with SIMDs); honours HIP/ROCR_VISIBLE_DEVICES."""
+    ids: List[int] = []
+    root = pathlib.Path("/sys/class/kfd/kfd/topology/nodes")
+    if root.exists():
+        gpus = []
+        for node in sorted(root.iterdir(), key=lambda p: int(p.name) if p.name.isdigit() else 1 << 30):
+            props = node / "properties"
+            try:
+                kv = dict(line.split() for line in props.read_text().splitlines() if len(line.split()) == 2)
+            except OSError:
+                continue
+            if int(kv.get("simd_count", "0")) > 0:
+                gpus.append(len(gpus))
+        ids = gpus
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis:
+        ids = [int(x) for x in vis.split(",") if x.strip().isdigit()]
+    return ids
+
+
+class _Task:
+    def __init__(self, cmd: Dict[str, Any]) -> None:
+        self.cmd = cmd
+        self.proc: Optional[subprocess.Popen] = None
+        self.killed = False
+
+
+class Agent:
+    def __init__(self, master_url: str, agent_id: Optional[str] = None, slots: Optional[int] = None,
+                 gpus: Optional[List[int]] = None, work_root: Optional[str] = None, host: Optional[str] = None,
+                 token: Optional[str] = None, label: str = "") -> None:
+        self.session = Session(master_url, token=token)
+        self.agent_id = agent_id or socket.gethostname()
+        self.gpus = detect_gpus() if gpus is None else gpus
+        self.use_gpu = bool(self.gpus) and slots is None
+        self.devices: List[Any] = list(self.gpus) if self.use_gpu else list(range(slots if slots is not None else 1))
+        self.work_root = pathlib.Path(work_root or os.path.join("/tmp", f"det-agent-{self.agent_id}"))
+        self.work_root.mkdir(parents=True, exist_ok=True)
+        self.host = host or "127.0.0.1"
+        self.label = label
+        self.tasks: Dict[str, _Task] = {}
+        self._stop = threading.Event()
+
+    def register(self) -> None:
+        self.session.post("/api/v1/agents/register", {"agent_id": self.agent_id, "slots": len(self.devices),
+                                                      "host": self.host, "devices": self.devices,
+                                                      "gpu": self.use_gpu, "label": self.label})
+        logger.info(f"agent {self.agent_id} registered {len(self.devices)} {'GPU' if self.use_gpu else 'CPU'} slots")
+
+    def run(self) -> None:
+        self.register()
+        while not self._stop.is_set():
+            try:
+                cmds = self.session.get(f"/api/v1/agents/{self.agent_id}/work", params={"timeout_seconds": 10},
+                                        timeout=40)["commands"]
+            except Exception as e:  # master restart / network blip: re-register
+                logger.warning(f"agent poll failed: {e}")
+                time.sleep(1)
+                try:
+                    self.register()
+                except Exception:
+                    pass
+                continue
+            for c in cmds:
+                if c["type"] == "start":
+                    threading.Thread(target=self._run_task, args=(c,), daemon=True).start()
+                elif c["type"] == "kill":
+                    self._kill(c["allocation_id"])
+
+    def stop(self) -> None:
+        self._stop.set()
+        for aid in list(self.tasks):
+            self._kill(aid)
+
+    # -- task execution ----------------------------------------------------------------------
+    def _prepare_workdir(self, c: Dict[str, Any]) -> pathlib.Path:
+        wd = self.work_root / c["allocation_id"]
+        wd.mkdir(parents=True, exist_ok=True)
+        b64 = None
+        if c.get("model_def_url"):
+            b64 = self.session.get(c["model_def_url"]).get("b64_tgz")
+        elif c.get("workdir_b64"):
+            b64 = c["workdir_b64"]
+        if b64:
+            with tarfile.open(fileobj=io.BytesIO(base64.b64decode(b64)), mode="r:gz") as tf:
+                tf.extractall(wd, filter="data")
+        return wd
+
+    @staticmethod
+    def _command(c: Dict[str, Any]) -> List[str]:
+        if c.get("command"):
+            cmd = c["command"]
+            return ["bash", "-c", cmd] if isinstance(cmd, str) else list(cmd)
+        ep = c.get("entrypoint")
+        if isinstance(ep, list):
+            return list(ep)
+        if ep and ":" in ep and " " not in ep.strip():
+            if int(c.get("slots_per_trial", 1)) > 1:
+                return [sys.executable, "-m", "determined_amd.launch.torch_distributed", "--trial", ep]
+            return [sys.executable, "-m", "determined_amd.exec.harness", ep]
+        if ep:
+            return ["bash", "-c", ep]
+        raise ValueError("task has neither an entrypoint nor a command")
+
+    def _run_task(self, c: Dict[str, Any]) -> None:
+        aid = c["allocation_id"]
+        t = _Task(c)
+        self.tasks[aid] = t
+        code = -1
+        try:
+            wd = self._prepare_workdir(c)
+            env = dict(os.environ)
+            env.update({k: str(v) for k, v in c.get("env", {}).items()})
+            env["DET_MODEL_DEF_DIR"] = str(wd)
+            env["PYTHONPATH"] = os.pathsep.join([str(wd), _repo_root()] + [p for p in [env.get("PYTHONPATH")] if p])
+            env["HSA_ENABLE_IPC_MODE_LEGACY"] = env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            devices = c.get("devices", [])
+            if c.get("gpu"):
+                env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+            else:
+                env["DET_CPU_SLOTS"] = str(len(devices))
+            argv = self._command(c)
+            self.session.post(f"/api/v1/agents/{self.agent_id}/events", {"type": "started", "allocation_id": aid})
+            t.proc = subprocess.Popen(argv, cwd=wd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      start_new_session=True, text=True, bufsize=1)
+            self._pump_logs(t, c["task_id"], aid)
+            code = t.proc.wait()
+        except Exception as e:
+            logger.exception(f"task {aid} failed to run")
+            self._ship(c["task_id"], aid, [f"agent: task failed to start: {e!r}"])
+        finally:
+            self.tasks.pop(aid, None)
+            try:
+                self.session.post(f"/api/v1/agents/{self.agent_id}/events",
+                                  {"type": "exited", "allocation_id": aid, "exit_code": code})
+            except Exception as e:
+                logger.warning(f"could not report exit of {aid}: {e}")
+
+    def _pump_logs(self, t: _Task, task_id: str, aid: str) -> None:
+        assert t.proc is not None and t.proc.stdout is not None
+        buf: List[str] = []
+        last = time.time()
+        for line in t.proc.stdout:
+            buf.append(line.rstrip("\n"))
+            if len(buf) >= 200 or time.time() - last > 0.5:
+                self._ship(task_id, aid, buf)
+                buf, last = [], time.time()
+        if buf:
+            self._ship(task_id, aid, buf)
+
+    def _ship(self, task_id: str, aid: str, lines: List[str]) -> None:
+        logs = []
+        for ln in lines:
+            rank = None
+            if ln.startswith("[rank=") and "]" in ln:
+                try:
+                    rank = int(ln[6:ln.index("]")])
+                except ValueError:
+                    pass
+            logs.append({"rank": rank, "log": ln})
+        try:
+            self.session.post("/api/v1/task/logs", {"task_id": task_id, "allocation_id": aid, "logs": logs})
+        except Exception as e:
+            logger.warning(f"log shipping failed: {e}")
+
+    def _kill(self, aid: str, grace: float = 10.0) -> None:
+        t = self.tasks.get(aid)
+        if t is None or t.proc is None:
+            return
+        t.killed = True
+        try:
+            os.killpg(t.proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            return
+
+        def hard() -> None:
+            time.sleep(grace)
+            if t.proc is not None and t.proc.poll() is None:
+                try:
+                    os.killpg(t.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+        threading.Thread(target=hard, daemon=True).start()
+
+
+def _repo_root() -> str:
+    return str(pathlib.Path(__file__).resolve().parents[2])

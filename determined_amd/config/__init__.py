@@ -1,0 +1,378 @@
+"""Experiment configuration ("expconf"): YAML/dict loading, defaults, validation, helpers.
+
+Mirrors the reference's v0 experiment schema (``schemas/expconf/v0/*.json``; Go defaults in
+``master/pkg/schemas/expconf``) -- same field names, same defaults, same length units --
+implemented as plain Python so the harness, master and CLI share one source of truth.
+"""
+
+import copy
+import enum
+import math
+import pathlib
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import yaml
+
+UNITS = ("batches", "records", "epochs")
+
+
+class InvalidConfig(ValueError):
+    def __init__(self, errors: List[str]) -> None:
+        super().__init__("invalid experiment config:\n  " + "\n  ".join(errors))
+        self.errors = errors
+
+
+class Unit(enum.Enum):
+    BATCHES = "batches"
+    RECORDS = "records"
+    EPOCHS = "epochs"
+
+
+class Length:
+    """A training length: ``{"batches": 100}`` / ``{"epochs": 2}`` / ``{"records": 6400}`` or a bare
+    int (unitless, used by the Core API / custom searchers)."""
+
+    __slots__ = ("unit", "units")
+
+    def __init__(self, unit: Optional[Unit], units: int) -> None:
+        self.unit = unit
+        self.units = int(units)
+
+    @classmethod
+    def parse(cls, v: Any) -> "Length":
+        if isinstance(v, Length):
+            return v
+        if isinstance(v, bool):
+            raise ValueError(f"invalid length {v!r}")
+        if isinstance(v, int):
+            return cls(None, v)
+        if isinstance(v, dict) and len(v) == 1:
+            (k, n), = v.items()
+            if k not in UNITS or not isinstance(n, int) or isinstance(n, bool) or n < 0:
+                raise ValueError(f"invalid length {v!r}")
+            return cls(Unit(k), n)
+        raise ValueError(f"invalid length {v!r}: expected an int or {{batches|records|epochs: N}}")
+
+    def to_batches(self, global_batch_size: int, records_per_epoch: Optional[int] = None) -> int:
+        if self.unit in (None, Unit.BATCHES):
+            return self.units
+        if self.unit == Unit.RECORDS:
+            return max(1, math.ceil(self.units / global_batch_size)) if self.units else 0
+        if not records_per_epoch:
+            raise ValueError("epoch lengths need records_per_epoch (or a sized training data loader)")
+        return max(1, math.ceil(self.units * records_per_epoch / global_batch_size)) if self.units else 0
+
+    def to_dict(self) -> Union[int, Dict[str, int]]:
+        return self.units if self.unit is None else {self.unit.value: self.units}
+
+    def __eq__(self, o: object) -> bool:
+        return isinstance(o, Length) and o.unit == self.unit and o.units == self.units
+
+    def __repr__(self) -> str:
+        return f"Length({self.to_dict()})"
+
+
+STORAGE_COMMON = {"save_experiment_best": 0, "save_trial_best": 1, "save_trial_latest": 1}
+STORAGE_DEFAULTS: Dict[str, Dict[str, Any]] = {
+    "shared_fs": {"host_path": None, "storage_path": None, "propagation": "rprivate", "container_path": None,
+                  "checkpoint_path": None, "tensorboard_path": None},
+    "directory": {"container_path": None},
+    "s3": {"access_key": None, "bucket": None, "secret_key": None, "endpoint_url": None, "prefix": None},
+    "gcs": {"bucket": None, "prefix": None},
+    "azure": {"container": None, "connection_string": None, "account_url": None, "credential": None},
+}
+
+SEARCHER_COMMON = {"metric": None, "smaller_is_better": True, "source_trial_id": None,
+                   "source_checkpoint_uuid": None}
+SEARCHER_DEFAULTS: Dict[str, Dict[str, Any]] = {
+    "single": {"max_length": None},
+    "random": {"max_concurrent_trials": 16, "max_trials": None, "max_length": None},
+    "grid": {"max_concurrent_trials": 16, "max_length": None},
+    "async_halving": {"num_rungs": None, "max_length": None, "max_trials": None, "divisor": 4,
+                      "max_concurrent_trials": 16, "stop_once": False},
+    "adaptive_asha": {"bracket_rungs": [], "max_trials": None, "mode": "standard", "divisor": 4, "max_rungs": 5,
+                      "max_concurrent_trials": 16, "max_length": None, "stop_once": False},
+    "custom": {"unit": None},
+}
+
+TOP_DEFAULTS: Dict[str, Any] = {
+    "bind_mounts": [],
+    "checkpoint_policy": "best",
+    "checkpoint_storage": None,
+    "data": {},
+    "debug": False,
+    "description": None,
+    "entrypoint": None,
+    "environment": {"image": {}, "environment_variables": [], "proxy_ports": [], "ports": {},
+                    "force_pull_image": False, "registry_auth": None, "add_capabilities": [],
+                    "drop_capabilities": [], "pod_spec": None},
+    "hyperparameters": {},
+    "labels": [],
+    "log_policies": [],
+    "retention_policy": None,
+    "max_restarts": 5,
+    "min_checkpoint_period": {"batches": 0},
+    "min_validation_period": {"batches": 0},
+    "name": None,
+    "optimizations": {"aggregation_frequency": 1, "auto_tune_tensor_fusion": False,
+                      "average_aggregated_gradients": True, "average_training_metrics": True,
+                      "gradient_compression": False, "grad_updates_size_file": None, "mixed_precision": "O0",
+                      "tensor_fusion_cycle_time": 1, "tensor_fusion_threshold": 64},
+    "perform_initial_validation": False,
+    "profiling": {"enabled": False, "begin_on_batch": 0, "end_after_batch": None, "sync_timings": True},
+    "project": "",
+    "records_per_epoch": 0,
+    "reproducibility": {"experiment_seed": None},
+    "resources": {"agent_label": None, "devices": [], "is_single_node": None, "max_slots": None,
+                  "native_parallel": False, "priority": None, "resource_pool": "", "shm_size": None,
+                  "slots_per_trial": 1, "weight": 1},
+    "scheduling_unit": 100,
+    "searcher": None,
+    "workspace": "",
+}
+
+HP_TYPES = ("const", "int", "double", "log", "categorical")
+CHECKPOINT_POLICIES = ("best", "all", "none")
+
+
+def _merge_defaults(cfg: Dict[str, Any], defaults: Dict[str, Any]) -> Dict[str, Any]:
+    for k, dv in defaults.items():
+        if k not in cfg or cfg[k] is None and dv is not None and isinstance(dv, dict):
+            cfg[k] = copy.deepcopy(dv)
+        elif isinstance(dv, dict) and isinstance(cfg.get(k), dict) and dv:
+            _merge_defaults(cfg[k], dv)
+    return cfg
+
+
+def load(src: Union[str, pathlib.Path, Dict[str, Any]]) -> Dict[str, Any]:
+    """Load a config from a YAML path, YAML text, or dict (no defaults applied)."""
+    if isinstance(src, dict):
+        return copy.deepcopy(src)
+    p = pathlib.Path(src) if not isinstance(src, str) or "\n" not in src else None
+    text = p.read_text() if p is not None and p.exists() else str(src)
+    out = yaml.safe_load(text)
+    if not isinstance(out, dict):
+        raise InvalidConfig(["config must be a mapping"])
+    return out
+
+
+def apply_defaults(cfg: Dict[str, Any], seed: Optional[int] = None) -> Dict[str, Any]:
+    """Fill every unset field with the reference schema default (returns a new dict)."""
+    cfg = copy.deepcopy(cfg)
+    _merge_defaults(cfg, TOP_DEFAULTS)
+    cs = cfg.get("checkpoint_storage")
+    if cs is None:
+        cs = cfg["checkpoint_storage"] = {"type": "shared_fs", "host_path": "/tmp/determined-checkpoints"}
+    if isinstance(cs, dict) and cs.get("type") in STORAGE_DEFAULTS:
+        _merge_defaults(cs, {**STORAGE_DEFAULTS[cs["type"]], **STORAGE_COMMON})
+    s = cfg.get("searcher")
+    if isinstance(s, dict) and s.get("name") in SEARCHER_DEFAULTS:
+        _merge_defaults(s, {**SEARCHER_DEFAULTS[s["name"]], **SEARCHER_COMMON})
+    if cfg.get("name") is None:
+        cfg["name"] = "Experiment (unnamed)"
+    if cfg["reproducibility"].get("experiment_seed") is None:
+        import random as _r
+
+        cfg["reproducibility"]["experiment_seed"] = seed if seed is not None else _r.randrange(2**31)
+    for name, hp in list(cfg.get("hyperparameters", {}).items()):
+        cfg["hyperparameters"][name] = normalize_hparam(hp)
+    return cfg
+
+
+def normalize_hparam(hp: Any) -> Any:
+    """Shorthand ``lr: 0.1`` -> ``{type: const, val: 0.1}``; nested dicts recurse."""
+    if isinstance(hp, dict):
+        if "type" in hp and hp["type"] in HP_TYPES:
+            out = dict(hp)
+            if out["type"] in ("int", "double", "log"):
+                out.setdefault("count", None)
+            return out
+        return {k: normalize_hparam(v) for k, v in hp.items()}
+    return {"type": "const", "val": hp}
+
+
+def _validate_hparam(path: str, hp: Any, errs: List[str]) -> None:
+    if not isinstance(hp, dict):
+        errs.append(f"{path}: hyperparameter must be a mapping")
+        return
+    t = hp.get("type")
+    if t is None:  # nested
+        for k, v in hp.items():
+            _validate_hparam(f"{path}.{k}", v, errs)
+        return
+    if t == "const":
+        if "val" not in hp:
+            errs.append(f"{path}: const hyperparameter needs 'val'")
+    elif t in ("int", "double", "log"):
+        for k in ("minval", "maxval"):
+            if k not in hp:
+                errs.append(f"{path}: {t} hyperparameter needs '{k}'")
+        if "minval" in hp and "maxval" in hp and hp["minval"] > hp["maxval"]:
+            errs.append(f"{path}: minval must be <= maxval")
+        if t == "int" and any(isinstance(hp.get(k), float) for k in ("minval", "maxval")):
+            errs.append(f"{path}: int hyperparameter bounds must be integers")
+        if t == "log" and "base" not in hp:
+            errs.append(f"{path}: log hyperparameter needs 'base'")
+        if hp.get("count") is not None and (not isinstance(hp["count"], int) or hp["count"] < 1):
+            errs.append(f"{path}: count must be a positive integer")
+    elif t == "categorical":
+        if not isinstance(hp.get("vals"), list) or not hp["vals"]:
+            errs.append(f"{path}: categorical hyperparameter needs a non-empty 'vals' list")
+    else:
+        errs.append(f"{path}: unknown hyperparameter type {t!r}")
+
+
+def validate(cfg: Dict[str, Any]) -> List[str]:
+    """Return a list of human-readable errors (empty if valid). Expects defaults applied."""
+    errs: List[str] = []
+    s = cfg.get("searcher")
+    if not isinstance(s, dict) or "name" not in s:
+        errs.append("searcher: required (with a 'name')")
+    else:
+        name = s["name"]
+        if name not in SEARCHER_DEFAULTS:
+            errs.append(f"searcher.name: unknown searcher {name!r} (one of {sorted(SEARCHER_DEFAULTS)})")
+        if not s.get("metric"):
+            errs.append("searcher.metric: required")
+        if name in ("single", "random", "grid", "async_halving", "adaptive_asha"):
+            if s.get("max_length") is None:
+                errs.append("searcher.max_length: required")
+            else:
+                try:
+                    Length.parse(s["max_length"])
+                except ValueError as e:
+                    errs.append(f"searcher.max_length: {e}")
+        if name in ("random", "async_halving", "adaptive_asha"):
+            mt = s.get("max_trials")
+            if not isinstance(mt, int) or mt < 1:
+                errs.append("searcher.max_trials: required positive integer")
+        if name == "async_halving" and not isinstance(s.get("num_rungs"), int):
+            errs.append("searcher.num_rungs: required for async_halving")
+        if name == "adaptive_asha" and s.get("mode") not in ("aggressive", "standard", "conservative"):
+            errs.append("searcher.mode: one of aggressive|standard|conservative")
+        if name in ("async_halving", "adaptive_asha") and not (s.get("divisor", 4) > 1):
+            errs.append("searcher.divisor: must be > 1")
+        if name == "grid":
+            for hname, hp in _flat_hparams(cfg.get("hyperparameters", {})):
+                if hp.get("type") in ("int", "double", "log") and hp.get("count") is None:
+                    errs.append(f"hyperparameters.{hname}: grid search needs 'count' for {hp['type']}")
+    hps = cfg.get("hyperparameters", {})
+    if not isinstance(hps, dict):
+        errs.append("hyperparameters: must be a mapping")
+    else:
+        for k, v in hps.items():
+            _validate_hparam(f"hyperparameters.{k}", v, errs)
+    cs = cfg.get("checkpoint_storage")
+    if not isinstance(cs, dict) or cs.get("type") not in STORAGE_DEFAULTS:
+        errs.append(f"checkpoint_storage.type: one of {sorted(STORAGE_DEFAULTS)}")
+    elif cs["type"] == "shared_fs" and not cs.get("host_path"):
+        errs.append("checkpoint_storage.host_path: required for shared_fs")
+    elif cs["type"] in ("s3", "gcs") and not cs.get("bucket"):
+        errs.append(f"checkpoint_storage.bucket: required for {cs['type']}")
+    elif cs["type"] == "directory" and not cs.get("container_path"):
+        errs.append("checkpoint_storage.container_path: required for directory")
+    for key in ("min_validation_period", "min_checkpoint_period"):
+        try:
+            Length.parse(cfg.get(key, {"batches": 0}))
+        except ValueError as e:
+            errs.append(f"{key}: {e}")
+    r = cfg.get("resources", {})
+    spt = r.get("slots_per_trial", 1)
+    if not isinstance(spt, int) or spt < 0:
+        errs.append("resources.slots_per_trial: must be a non-negative integer")
+    if r.get("max_slots") is not None and r["max_slots"] < spt:
+        errs.append("resources.max_slots: must be >= slots_per_trial")
+    if cfg.get("checkpoint_policy") not in CHECKPOINT_POLICIES:
+        errs.append(f"checkpoint_policy: one of {CHECKPOINT_POLICIES}")
+    if not isinstance(cfg.get("max_restarts", 0), int) or cfg.get("max_restarts", 0) < 0:
+        errs.append("max_restarts: must be a non-negative integer")
+    opt = cfg.get("optimizations", {})
+    if not isinstance(opt.get("aggregation_frequency", 1), int) or opt.get("aggregation_frequency", 1) < 1:
+        errs.append("optimizations.aggregation_frequency: must be >= 1")
+    if not isinstance(cfg.get("scheduling_unit", 100), int) or cfg.get("scheduling_unit", 100) < 1:
+        errs.append("scheduling_unit: must be >= 1")
+    return errs
+
+
+def _flat_hparams(hps: Dict[str, Any], prefix: str = "") -> List[Tuple[str, Dict[str, Any]]]:
+    out = []
+    for k, v in hps.items():
+        if isinstance(v, dict) and "type" not in v:
+            out += _flat_hparams(v, f"{prefix}{k}.")
+        else:
+            out.append((prefix + k, v))
+    return out
+
+
+def parse(src: Union[str, pathlib.Path, Dict[str, Any]], seed: Optional[int] = None) -> Dict[str, Any]:
+    """load + apply_defaults + validate; raises InvalidConfig."""
+    cfg = apply_defaults(load(src), seed=seed)
+    errs = validate(cfg)
+    if errs:
+        raise InvalidConfig(errs)
+    return cfg
+
+
+def searcher_unit(cfg: Dict[str, Any]) -> Optional[Unit]:
+    s = cfg.get("searcher", {}) or {}
+    if s.get("unit"):
+        return Unit(s["unit"])
+    ml = s.get("max_length")
+    if isinstance(ml, dict) and len(ml) == 1:
+        return Unit(next(iter(ml)))
+    return None
+
+
+def global_batch_size(cfg: Dict[str, Any], hparams: Optional[Dict[str, Any]] = None) -> Optional[int]:
+    hp = hparams if hparams is not None else {
+        k: v.get("val") for k, v in cfg.get("hyperparameters", {}).items() if isinstance(v, dict)
+    }
+    gbs = hp.get("global_batch_size")
+    return int(gbs) if gbs is not None else None
+
+
+class ExperimentConfig(dict):
+    """Dict with convenience accessors (reference: ``harness/determined/_experiment_config.py``)."""
+
+    def debug_enabled(self) -> bool:
+        return bool(self.get("debug", False))
+
+    def scheduling_unit(self) -> int:
+        return int(self.get("scheduling_unit", 100))
+
+    def native_parallel_enabled(self) -> bool:
+        return bool(self.get("resources", {}).get("native_parallel", False))
+
+    def averaging_training_metrics_enabled(self) -> bool:
+        return bool(self.get("optimizations", {}).get("average_training_metrics", True))
+
+    def slots_per_trial(self) -> int:
+        return int(self.get("resources", {}).get("slots_per_trial", 1))
+
+    def experiment_seed(self) -> int:
+        return int(self.get("reproducibility", {}).get("experiment_seed") or 0)
+
+    def profiling_enabled(self) -> bool:
+        return bool(self.get("profiling", {}).get("enabled", False))
+
+    def profiling_interval(self) -> Tuple[int, Optional[int]]:
+        p = self.get("profiling", {})
+        return int(p.get("begin_on_batch", 0)), p.get("end_after_batch")
+
+    def get_records_per_epoch(self) -> int:
+        return int(self.get("records_per_epoch", 0) or 0)
+
+    def get_min_validation_period(self) -> Dict[str, int]:
+        return self.get("min_validation_period", {"batches": 0})
+
+    def get_min_checkpoint_period(self) -> Dict[str, int]:
+        return self.get("min_checkpoint_period", {"batches": 0})
+
+    def get_searcher_metric(self) -> str:
+        return self["searcher"]["metric"]
+
+    def get_optimizations_config(self) -> Dict[str, Any]:
+        return self.get("optimizations", {})
+
+    def get_checkpoint_storage(self) -> Dict[str, Any]:
+        return self.get("checkpoint_storage", {})

@@ -1,0 +1,841 @@
+"""The master's state machines (reference: ``master/internal/{experiment,trial,checkpoint_gc}.go``,
+``master/internal/task`` allocations/preemption, ``master/internal/rm/agentrm`` resource manager).
+
+One process, one global lock.  Experiments own a searcher (native C++ engine or a custom
+searcher event queue); each searcher ``create`` becomes a trial, each ``validate_after`` is
+queued on its trial, ``close`` ends it.  Trials with work and no allocation request slots from
+the native scheduler; allocations are dispatched to agents, which launch the harness.
+"""
+
+import base64
+import json
+import logging
+import os
+import threading
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Tuple
+
+from determined_amd import config as expconf
+from determined_amd.master._db import DB
+
+logger = logging.getLogger("determined_amd.master")
+
+TERMINAL_EXP = {"COMPLETED", "CANCELED", "ERROR", "DELETED"}
+TERMINAL_TRIAL = {"COMPLETED", "CANCELED", "ERROR"}
+
+
+class Allocation:
+    def __init__(self, alloc_id: str, task_id: str, slots: int, exp_id: Optional[int] = None,
+                 trial_id: Optional[int] = None, kind: str = "TRIAL") -> None:
+        self.id = alloc_id
+        self.task_id = task_id
+        self.slots = slots
+        self.exp_id = exp_id
+        self.trial_id = trial_id
+        self.kind = kind
+        self.state = "PENDING"
+        self.assignment: List[Tuple[str, List[int]]] = []
+        self.preempt = False
+        self.ack_preempt = False
+        self.killed = False
+        self.exit_codes: Dict[str, int] = {}
+        self.start_time = time.time()
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {"allocation_id": self.id, "task_id": self.task_id, "slots": self.slots, "state": self.state,
+                "assignment": self.assignment, "preempt": self.preempt, "killed": self.killed,
+                "trial_id": self.trial_id, "experiment_id": self.exp_id}
+
+
+class TrialRec:
+    def __init__(self, tid: int, exp_id: int, request_id: int, hparams: Dict[str, Any], seed: int) -> None:
+        self.id = tid
+        self.exp_id = exp_id
+        self.request_id = request_id
+        self.hparams = hparams
+        self.seed = seed
+        self.state = "ACTIVE"
+        self.ops: List[int] = []
+        self.close_requested = False
+        self.restarts = 0
+        self.run_id = 0
+        self.allocation: Optional[Allocation] = None
+        self.latest_checkpoint: Optional[str] = None
+        self.total_batches = 0
+        self.early_exit: Optional[str] = None
+        self.warm_start: Optional[str] = None
+
+    def searcher_state(self) -> Dict[str, Any]:
+        return {"ops": self.ops, "close_requested": self.close_requested, "early_exit": self.early_exit}
+
+
+class ExperimentRec:
+    def __init__(self, eid: int, cfg: Dict[str, Any], state: str) -> None:
+        self.id = eid
+        self.config = cfg
+        self.state = state
+        self.searcher: Any = None
+        self.custom_events: List[Dict[str, Any]] = []
+        self.custom_event_id = 0
+        self.trials: Dict[int, TrialRec] = {}  # request_id -> trial
+        self.shutdown = False
+        self.progress = 0.0
+
+
+class Master:
+    def __init__(self, db_path: str = ":memory:", policy: str = "priority", fit: str = "best",
+                 preemption: bool = True, cluster_id: Optional[str] = None, master_url: str = "http://127.0.0.1:8080",
+                 auth_token: Optional[str] = None) -> None:
+        from determined_amd._native import load
+
+        self.native = load()
+        self.lock = threading.RLock()
+        self.cv = threading.Condition(self.lock)
+        self.db = DB(db_path)
+        pol = {"priority": self.native.Policy.PRIORITY, "fair_share": self.native.Policy.FAIR_SHARE,
+               "round_robin": self.native.Policy.ROUND_ROBIN}[policy]
+        self.policy = policy
+        self.sched = self.native.Scheduler(pol, self.native.Fit.BEST if fit == "best" else self.native.Fit.WORST,
+                                           preemption)
+        self.cluster_id = cluster_id or str(uuid.uuid4())
+        self.master_url = master_url
+        self.auth_token = auth_token
+        self.agents: Dict[str, Dict[str, Any]] = {}
+        self.allocations: Dict[str, Allocation] = {}
+        self.experiments: Dict[int, ExperimentRec] = {}
+        self._order = 0
+        self._closed = False
+        self._restore()
+        self._ticker = threading.Thread(target=self._tick_loop, daemon=True, name="master-tick")
+        self._ticker.start()
+
+    # ================================================================ lifecycle / restore
+    def close(self) -> None:
+        with self.lock:
+            self._closed = True
+            self.cv.notify_all()
+
+    def _tick_loop(self) -> None:
+        while True:
+            with self.lock:
+                if self._closed:
+                    return
+                self._check_agents()
+                self._schedule()
+                self.cv.wait(1.0)
+
+    def _restore(self) -> None:
+        for row in self.db.all("SELECT * FROM experiments WHERE state IN ('ACTIVE','PAUSED','STOPPING_CANCELED',"
+                               "'STOPPING_COMPLETED')"):
+            cfg = row["config"]
+            exp = ExperimentRec(row["id"], cfg, row["state"])
+            self.experiments[exp.id] = exp
+            if cfg["searcher"]["name"] != "custom":
+                from determined_amd.searcher import Searcher
+
+                exp.searcher = Searcher(cfg["searcher"], cfg.get("hyperparameters", {}),
+                                        cfg["reproducibility"]["experiment_seed"])
+                if row.get("searcher_snapshot"):
+                    exp.searcher.restore(row["searcher_snapshot"])
+            for t in self.db.all("SELECT * FROM trials WHERE experiment_id=?", [exp.id]):
+                tr = TrialRec(t["id"], exp.id, t["request_id"], t["hparams"], t["seed"])
+                tr.state = t["state"]
+                tr.restarts = t["restarts"] or 0
+                tr.run_id = t["run_id"] or 0
+                tr.latest_checkpoint = t["latest_checkpoint"]
+                tr.total_batches = t["total_batches"] or 0
+                ss = t.get("searcher_state") or {}
+                tr.ops = list(ss.get("ops", []))
+                tr.close_requested = bool(ss.get("close_requested", False))
+                tr.early_exit = ss.get("early_exit")
+                tr.warm_start = t.get("warm_start_checkpoint")
+                exp.trials[tr.request_id] = tr
+                if exp.state == "ACTIVE" and tr.state == "ACTIVE" and tr.ops:
+                    self._request_allocation(exp, tr)
+            self._order = max(self._order, exp.id * 1000)
+
+    # ================================================================ experiments
+    def create_experiment(self, cfg: Dict[str, Any], model_def: Optional[bytes], activate: bool = True,
+                          parent_id: Optional[int] = None, unmanaged: bool = False) -> int:
+        cfg = expconf.parse(cfg)
+        with self.lock:
+            eid = self.db.insert("experiments", name=cfg["name"], state="ACTIVE" if activate else "PAUSED",
+                                 config=cfg, model_def=model_def, parent_id=parent_id, start_time=time.time(),
+                                 description=cfg.get("description") or "", labels=cfg.get("labels") or [],
+                                 unmanaged=int(unmanaged), project=cfg.get("project") or "Uncategorized",
+                                 workspace=cfg.get("workspace") or "Uncategorized")
+            exp = ExperimentRec(eid, cfg, "ACTIVE" if activate else "PAUSED")
+            self.experiments[eid] = exp
+            if cfg["searcher"]["name"] == "custom":
+                self._custom_event(exp, {"initial_operations": {}})
+            else:
+                from determined_amd.searcher import Searcher
+
+                exp.searcher = Searcher(cfg["searcher"], cfg.get("hyperparameters", {}),
+                                        cfg["reproducibility"]["experiment_seed"])
+                self._process_ops(exp, exp.searcher.initial_operations())
+            self._persist_exp(exp)
+            self._fire_webhooks(exp, "EXPERIMENT_STATE_CHANGE")
+            self.cv.notify_all()
+            return eid
+
+    def _persist_exp(self, exp: ExperimentRec) -> None:
+        snap = exp.searcher.snapshot() if exp.searcher is not None else None
+        if exp.searcher is not None:
+            try:
+                exp.progress = exp.searcher.progress()
+            except Exception:
+                pass
+        self.db.update("experiments", "id", exp.id, state=exp.state, searcher_snapshot=snap, progress=exp.progress)
+
+    def _persist_trial(self, tr: TrialRec) -> None:
+        self.db.update("trials", "id", tr.id, state=tr.state, restarts=tr.restarts, run_id=tr.run_id,
+                       latest_checkpoint=tr.latest_checkpoint, total_batches=tr.total_batches,
+                       searcher_state=tr.searcher_state(),
+                       end_time=time.time() if tr.state in TERMINAL_TRIAL else None)
+
+    def _process_ops(self, exp: ExperimentRec, ops: List[Dict[str, Any]]) -> None:
+        """Apply searcher operations (reference experiment.go:processOperations)."""
+        queue = list(ops)
+        while queue:
+            op = queue.pop(0)
+            t = op["type"]
+            rid = op.get("request_id")
+            if t == "create":
+                seed = (exp.config["reproducibility"]["experiment_seed"] + len(exp.trials)) % (2**31)
+                tid = self.db.insert("trials", experiment_id=exp.id, request_id=rid, state="ACTIVE",
+                                     hparams=op["hparams"], seed=seed, start_time=time.time(),
+                                     warm_start_checkpoint=op.get("checkpoint"))
+                tr = TrialRec(tid, exp.id, rid, op["hparams"], seed)
+                tr.warm_start = op.get("checkpoint") or exp.config["searcher"].get("source_checkpoint_uuid")
+                exp.trials[rid] = tr
+                if exp.searcher is not None:
+                    queue += exp.searcher.trial_created(rid)
+                else:
+                    self._custom_event(exp, {"trial_created": {"request_id": rid}})
+            elif t == "validate_after":
+                tr = exp.trials.get(rid)
+                if tr is None or tr.state in TERMINAL_TRIAL:
+                    continue
+                tr.ops.append(int(op["length"]))
+                self._persist_trial(tr)
+                if tr.allocation is None and exp.state == "ACTIVE":
+                    self._request_allocation(exp, tr)
+            elif t == "close":
+                tr = exp.trials.get(rid)
+                if tr is None or tr.state in TERMINAL_TRIAL:
+                    continue
+                tr.close_requested = True
+                self._persist_trial(tr)
+                if tr.allocation is None and not tr.ops:
+                    queue += self._finish_trial(exp, tr, "COMPLETED")
+            elif t == "shutdown":
+                exp.shutdown = True
+                if op.get("cancel"):
+                    self._stop_experiment(exp, "CANCELED")
+                elif op.get("failure"):
+                    self._stop_experiment(exp, "ERROR")
+            elif t == "progress":
+                exp.progress = float(op.get("progress", 0.0))
+        self._maybe_complete(exp)
+        self._persist_exp(exp)
+
+    def _finish_trial(self, exp: ExperimentRec, tr: TrialRec, state: str) -> List[Dict[str, Any]]:
+        if tr.state in TERMINAL_TRIAL:
+            return []
+        tr.state = state
+        self._persist_trial(tr)
+        self._fire_webhooks(exp, "TRIAL_STATE_CHANGE", trial=tr)
+        if exp.searcher is None:
+            if state == "COMPLETED" and not tr.early_exit:
+                self._custom_event(exp, {"trial_closed": {"request_id": tr.request_id}})
+            else:
+                self._custom_event(exp, {"trial_exited_early": {"request_id": tr.request_id,
+                                                                "exited_reason": tr.early_exit or "errored"}})
+            return []
+        if state == "COMPLETED" and not tr.early_exit:
+            return exp.searcher.trial_closed(tr.request_id)
+        reason = tr.early_exit or ("user_canceled" if state == "CANCELED" else "errored")
+        return exp.searcher.trial_exited_early(tr.request_id, reason)
+
+    def _maybe_complete(self, exp: ExperimentRec) -> None:
+        if exp.state in TERMINAL_EXP:
+            return
+        active = [t for t in exp.trials.values() if t.state not in TERMINAL_TRIAL]
+        if exp.state in ("STOPPING_CANCELED", "STOPPING_ERROR") and not any(t.allocation for t in active):
+            for t in active:
+                t.state = "CANCELED"
+                self._persist_trial(t)
+            self._set_exp_state(exp, "CANCELED" if exp.state == "STOPPING_CANCELED" else "ERROR")
+            return
+        if exp.searcher is None and not exp.shutdown:
+            return
+        if not active and exp.trials:
+            all_err = all(t.state == "ERROR" for t in exp.trials.values())
+            self._set_exp_state(exp, "ERROR" if all_err else "COMPLETED")
+        elif exp.shutdown and not active:
+            self._set_exp_state(exp, "COMPLETED")
+
+    def _set_exp_state(self, exp: ExperimentRec, state: str) -> None:
+        exp.state = state
+        self.db.update("experiments", "id", exp.id, state=state,
+                       end_time=time.time() if state in TERMINAL_EXP else None)
+        self._fire_webhooks(exp, "EXPERIMENT_STATE_CHANGE")
+        if state in TERMINAL_EXP:
+            exp.progress = 1.0 if state == "COMPLETED" else exp.progress
+            self._persist_exp(exp)
+            threading.Thread(target=self.gc_experiment_checkpoints, args=(exp.id,), daemon=True).start()
+            self._custom_event(exp, {"experiment_inactive": {"experiment_state": state}})
+        self.cv.notify_all()
+
+    def _stop_experiment(self, exp: ExperimentRec, final: str) -> None:
+        exp.state = "STOPPING_CANCELED" if final == "CANCELED" else "STOPPING_ERROR"
+        for tr in exp.trials.values():
+            if tr.allocation is not None:
+                self._kill_allocation(tr.allocation)
+        self._maybe_complete(exp)
+
+    def pause_experiment(self, eid: int) -> None:
+        with self.lock:
+            exp = self._exp(eid)
+            if exp.state != "ACTIVE":
+                return
+            self._set_exp_state(exp, "PAUSED")
+            for tr in exp.trials.values():
+                a = tr.allocation
+                if a is not None:
+                    if a.state == "PENDING":
+                        self._drop_allocation(a)
+                        tr.allocation = None
+                    else:
+                        a.preempt = True
+            self.cv.notify_all()
+
+    def activate_experiment(self, eid: int) -> None:
+        with self.lock:
+            exp = self._exp(eid)
+            if exp.state != "PAUSED":
+                return
+            self._set_exp_state(exp, "ACTIVE")
+            for tr in exp.trials.values():
+                if tr.state == "ACTIVE" and tr.ops and tr.allocation is None:
+                    self._request_allocation(exp, tr)
+            self.cv.notify_all()
+
+    def kill_experiment(self, eid: int) -> None:
+        with self.lock:
+            exp = self._exp(eid)
+            if exp.state in TERMINAL_EXP:
+                return
+            self._stop_experiment(exp, "CANCELED")
+            self.cv.notify_all()
+
+    def archive_experiment(self, eid: int, archived: bool = True) -> None:
+        with self.lock:
+            self.db.update("experiments", "id", eid, archived=int(archived))
+
+    def delete_experiment(self, eid: int) -> None:
+        with self.lock:
+            exp = self.experiments.get(eid)
+            if exp is not None and exp.state not in TERMINAL_EXP:
+                raise ValueError("only terminal experiments can be deleted")
+            self.gc_experiment_checkpoints(eid, delete_all=True)
+            self.db.update("experiments", "id", eid, state="DELETED")
+
+    def _exp(self, eid: int) -> ExperimentRec:
+        exp = self.experiments.get(eid)
+        if exp is None:
+            row = self.db.one("SELECT id, state, config FROM experiments WHERE id=?", [eid])
+            if row is None:
+                raise KeyError(f"experiment {eid} not found")
+            exp = ExperimentRec(eid, row["config"], row["state"])
+        return exp
+
+    def _trial(self, tid: int) -> Tuple[ExperimentRec, TrialRec]:
+        for exp in self.experiments.values():
+            for tr in exp.trials.values():
+                if tr.id == tid:
+                    return exp, tr
+        raise KeyError(f"trial {tid} not active")
+
+    # ================================================================ allocations
+    def _next_order(self) -> int:
+        self._order += 1
+        return self._order
+
+    def _request_allocation(self, exp: ExperimentRec, tr: TrialRec) -> None:
+        slots = int(exp.config["resources"].get("slots_per_trial", 1))
+        aid = f"trial-{tr.id}.{tr.run_id + 1}.{uuid.uuid4().hex[:6]}"
+        a = Allocation(aid, f"trial-{tr.id}", slots, exp.id, tr.id)
+        tr.allocation = a
+        self.allocations[aid] = a
+        prio = exp.config["resources"].get("priority")
+        self.sched.add_request(aid, f"exp-{exp.id}", slots, int(prio) if prio is not None else 42,
+                               float(exp.config["resources"].get("weight", 1)), self._next_order(), True)
+        self.cv.notify_all()
+
+    def create_command(self, cmd: List[str], slots: int = 0, env: Optional[Dict[str, str]] = None,
+                       kind: str = "COMMAND", workdir_b64: Optional[str] = None) -> str:
+        with self.lock:
+            task_id = f"{kind.lower()}-{uuid.uuid4().hex[:8]}"
+            aid = f"{task_id}.1"
+            a = Allocation(aid, task_id, slots, kind=kind)
+            a.command = cmd  # type: ignore[attr-defined]
+            a.env = env or {}  # type: ignore[attr-defined]
+            a.workdir_b64 = workdir_b64  # type: ignore[attr-defined]
+            self.allocations[aid] = a
+            self.db.insert("tasks", id=task_id, type=kind, state="PENDING", config={"cmd": cmd, "slots": slots},
+                           start_time=time.time())
+            self.sched.add_request(aid, task_id, slots, 42, 1.0, self._next_order(), False)
+            self.cv.notify_all()
+            return task_id
+
+    def _drop_allocation(self, a: Allocation) -> None:
+        self.sched.remove_request(a.id)
+        a.state = "TERMINATED"
+        self.cv.notify_all()
+
+    def _kill_allocation(self, a: Allocation) -> None:
+        a.killed = True
+        if a.state == "PENDING":
+            self._drop_allocation(a)
+            self._on_allocation_exit(a)
+            return
+        for agent_id, _ in a.assignment:
+            ag = self.agents.get(agent_id)
+            if ag is not None:
+                ag["queue"].append({"type": "kill", "allocation_id": a.id})
+        a.state = "TERMINATING"
+        self.cv.notify_all()
+
+    def kill_task(self, task_id: str) -> None:
+        with self.lock:
+            for a in list(self.allocations.values()):
+                if a.task_id == task_id and a.state != "TERMINATED":
+                    self._kill_allocation(a)
+
+    def _schedule(self) -> None:
+        d = self.sched.schedule()
+        reqs = None
+        for aid in d["allocated"]:
+            a = self.allocations.get(aid)
+            if a is None:
+                continue
+            reqs = reqs or self.sched.requests()
+            a.assignment = [(ag, list(sl)) for ag, sl in reqs[aid]["assignment"]]
+            a.state = "ASSIGNED"
+            self._dispatch(a)
+        for aid in d["preempt"]:
+            a = self.allocations.get(aid)
+            if a is not None:
+                a.preempt = True
+        if d["allocated"] or d["preempt"]:
+            self.cv.notify_all()
+
+    def _dispatch(self, a: Allocation) -> None:
+        hosts = [self.agents[ag]["host"] for ag, _ in a.assignment]
+        for rank, (agent_id, slots) in enumerate(a.assignment):
+            ag = self.agents[agent_id]
+            devices = [ag["devices"][s] for s in slots] if ag.get("devices") else slots
+            env = {
+                "DET_MASTER": self.master_url,
+                "DET_CLUSTER_ID": self.cluster_id,
+                "DET_AGENT_ID": agent_id,
+                "DET_ALLOCATION_ID": a.id,
+                "DET_TASK_ID": a.task_id,
+                "DET_SESSION_TOKEN": self.auth_token or "",
+                "DET_SLOT_IDS": json.dumps(devices),
+                "DET_CONTAINER_ADDRS": json.dumps(hosts),
+                "DET_CONTAINER_RANK": str(rank),
+                "DET_TASK_TYPE": a.kind,
+                "DET_USE_GPU": "1" if ag.get("gpu") else "0",
+            }
+            cmd: Dict[str, Any] = {"type": "start", "allocation_id": a.id, "task_id": a.task_id, "devices": devices,
+                                   "gpu": bool(ag.get("gpu")), "env": env}
+            if a.kind == "TRIAL":
+                exp = self.experiments[a.exp_id]  # type: ignore[index]
+                tr = next(t for t in exp.trials.values() if t.id == a.trial_id)
+                tr.run_id += 1
+                cfg = exp.config
+                env.update({
+                    "DET_TRIAL_ID": str(tr.id),
+                    "DET_EXPERIMENT_ID": str(exp.id),
+                    "DET_TRIAL_SEED": str(tr.seed),
+                    "DET_HPARAMS": json.dumps(tr.hparams),
+                    "DET_EXPERIMENT_CONFIG": json.dumps(cfg),
+                    "DET_STEPS_COMPLETED": str(tr.total_batches),
+                    "DET_TRIAL_RUN_ID": str(tr.run_id),
+                    "DET_LATEST_CHECKPOINT": tr.latest_checkpoint or tr.warm_start or "",
+                })
+                for kv in _env_list(cfg.get("environment", {}).get("environment_variables")):
+                    k, _, v = kv.partition("=")
+                    env[k] = v
+                cmd.update(entrypoint=cfg.get("entrypoint"), slots_per_trial=a.slots,
+                           model_def_url=f"/api/v1/experiments/{exp.id}/model_def")
+                self._persist_trial(tr)
+            else:
+                cmd.update(command=getattr(a, "command", []), workdir_b64=getattr(a, "workdir_b64", None))
+                env.update(getattr(a, "env", {}))
+                self.db.update("tasks", "id", a.task_id, state="RUNNING")
+            ag["queue"].append(cmd)
+        self.cv.notify_all()
+
+    # ================================================================ agents
+    def register_agent(self, agent_id: str, slots: int, host: str = "127.0.0.1", devices: Optional[List[Any]] = None,
+                       gpu: bool = False, label: str = "") -> Dict[str, Any]:
+        with self.lock:
+            existing = self.agents.get(agent_id)
+            self.agents[agent_id] = {"id": agent_id, "slots": slots, "host": host, "devices": devices or list(range(slots)),
+                                     "gpu": gpu, "label": label, "queue": existing["queue"] if existing else [],
+                                     "last_seen": time.time(), "enabled": True}
+            if existing is None:
+                self.sched.add_agent(agent_id, slots)
+            self.cv.notify_all()
+            return {"cluster_id": self.cluster_id}
+
+    def agent_poll(self, agent_id: str, timeout: float) -> List[Dict[str, Any]]:
+        deadline = time.time() + timeout
+        with self.lock:
+            ag = self.agents.get(agent_id)
+            if ag is None:
+                raise KeyError(f"agent {agent_id} not registered")
+            while not ag["queue"] and time.time() < deadline and not self._closed:
+                ag["last_seen"] = time.time()
+                self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
+            ag["last_seen"] = time.time()
+            out, ag["queue"] = ag["queue"], []
+            return out
+
+    def _check_agents(self, stale_s: float = 120.0) -> None:
+        now = time.time()
+        for aid, ag in list(self.agents.items()):
+            if now - ag["last_seen"] > stale_s:
+                logger.warning(f"agent {aid} lost")
+                self.sched.remove_agent(aid)
+                del self.agents[aid]
+                for a in list(self.allocations.values()):
+                    if any(x[0] == aid for x in a.assignment) and a.state in ("ASSIGNED", "RUNNING"):
+                        a.exit_codes[aid] = -1
+                        self._finish_allocation(a)
+
+    def agent_event(self, agent_id: str, ev: Dict[str, Any]) -> None:
+        with self.lock:
+            a = self.allocations.get(ev["allocation_id"])
+            if a is None:
+                return
+            if ev["type"] == "started":
+                a.state = "RUNNING"
+                if a.kind != "TRIAL":
+                    pass
+            elif ev["type"] == "exited":
+                a.exit_codes[agent_id] = int(ev.get("exit_code", -1))
+                if len(a.exit_codes) >= len(a.assignment):
+                    self._finish_allocation(a)
+            self.cv.notify_all()
+
+    def _finish_allocation(self, a: Allocation) -> None:
+        if a.state == "TERMINATED":
+            return
+        self.sched.remove_request(a.id)
+        a.state = "TERMINATED"
+        self._on_allocation_exit(a)
+        self.cv.notify_all()
+
+    def _on_allocation_exit(self, a: Allocation) -> None:
+        ok = all(c == 0 for c in a.exit_codes.values()) and bool(a.exit_codes)
+        if a.kind != "TRIAL":
+            code = max(a.exit_codes.values()) if a.exit_codes else -1
+            self.db.update("tasks", "id", a.task_id, state="TERMINATED" if not a.killed else "CANCELED",
+                           end_time=time.time(), exit_code=code)
+            return
+        exp = self.experiments.get(a.exp_id)  # type: ignore[arg-type]
+        if exp is None:
+            return
+        try:
+            _, tr = self._trial(a.trial_id)  # type: ignore[arg-type]
+        except KeyError:
+            return
+        tr.allocation = None
+        ops: List[Dict[str, Any]] = []
+        if a.killed or exp.state in ("STOPPING_CANCELED", "STOPPING_ERROR"):
+            ops = self._finish_trial(exp, tr, "CANCELED")
+        elif tr.early_exit:
+            ops = self._finish_trial(exp, tr, "COMPLETED")
+        elif ok or (a.preempt and a.ack_preempt):
+            if tr.close_requested and not tr.ops:
+                ops = self._finish_trial(exp, tr, "COMPLETED")
+            elif tr.ops and exp.state == "ACTIVE":
+                self._request_allocation(exp, tr)
+            # else: waiting for the searcher (e.g. an ASHA promotion) or paused
+        else:
+            tr.restarts += 1
+            max_restarts = int(exp.config.get("max_restarts", 5))
+            logger.warning(f"trial {tr.id} failed (exit {a.exit_codes}); restart {tr.restarts}/{max_restarts}")
+            if tr.restarts > max_restarts:
+                ops = self._finish_trial(exp, tr, "ERROR")
+            elif exp.state == "ACTIVE":
+                self._request_allocation(exp, tr)
+        self._persist_trial(tr)
+        self._process_ops(exp, ops)
+
+    # ================================================================ harness-facing
+    def get_searcher_op(self, tid: int) -> Dict[str, Any]:
+        with self.lock:
+            _, tr = self._trial(tid)
+            if tr.ops:
+                return {"completed": False, "op": {"validate_after": {"length": tr.ops[0]}}}
+            return {"completed": True, "op": None}
+
+    def complete_searcher_op(self, tid: int, length: int, metric: Any) -> None:
+        with self.lock:
+            exp, tr = self._trial(tid)
+            if not tr.ops or tr.ops[0] != int(length):
+                raise ValueError(f"trial {tid} has no pending operation of length {length} (pending {tr.ops})")
+            tr.ops.pop(0)
+            self.db.update("trials", "id", tid, searcher_metric=float(metric) if _isnum(metric) else None)
+            self._persist_trial(tr)
+            if exp.searcher is not None:
+                ops = exp.searcher.validation_completed(tr.request_id, float(metric), int(length))
+                self._process_ops(exp, ops)
+            else:
+                self._custom_event(exp, {"validation_completed": {"request_id": tr.request_id, "metric": metric,
+                                                                  "validate_after_length": int(length)}})
+            self.cv.notify_all()
+
+    def report_progress(self, tid: int, progress: float) -> None:
+        with self.lock:
+            exp, tr = self._trial(tid)
+            if exp.searcher is not None:
+                exp.searcher.set_trial_progress(tr.request_id, progress)
+                exp.progress = exp.searcher.progress()
+                self.db.update("experiments", "id", exp.id, progress=exp.progress)
+
+    def report_metrics(self, tid: int, body: Dict[str, Any]) -> None:
+        with self.lock:
+            group = body["group"]
+            self.db.insert("metrics", trial_id=tid, trial_run_id=body.get("trial_run_id", 0), group_name=group,
+                           steps_completed=int(body["steps_completed"]), metrics=body["metrics"],
+                           batch_metrics=body.get("batch_metrics"), ts=time.time())
+            if group in ("training", "validation"):
+                try:
+                    exp, tr = self._trial(tid)
+                    tr.total_batches = max(tr.total_batches, int(body["steps_completed"]))
+                    self._persist_trial(tr)
+                    if group == "validation":
+                        m = exp.config["searcher"].get("metric")
+                        v = body["metrics"].get(m)
+                        if _isnum(v):
+                            row = self.db.one("SELECT best_validation FROM trials WHERE id=?", [tid])
+                            sib = exp.config["searcher"].get("smaller_is_better", True)
+                            best = row["best_validation"] if row else None
+                            if best is None or (v < best if sib else v > best):
+                                self.db.update("trials", "id", tid, best_validation=float(v))
+                except KeyError:
+                    pass
+
+    def report_checkpoint(self, body: Dict[str, Any]) -> None:
+        with self.lock:
+            tid = body.get("trial_id")
+            exp_id = None
+            metric = None
+            steps = body.get("steps_completed") or (body.get("metadata") or {}).get("steps_completed")
+            if tid is not None:
+                try:
+                    exp, tr = self._trial(int(tid))
+                    exp_id = exp.id
+                    tr.latest_checkpoint = body["uuid"]
+                    if steps is not None:
+                        tr.total_batches = max(tr.total_batches, int(steps))
+                    self._persist_trial(tr)
+                    m = exp.config["searcher"].get("metric")
+                    row = self.db.one("SELECT metrics FROM metrics WHERE trial_id=? AND group_name='validation' "
+                                      "AND steps_completed=? ORDER BY id DESC", [tid, steps])
+                    if row and _isnum((row["metrics"] or {}).get(m)):
+                        metric = float(row["metrics"][m])
+                except KeyError:
+                    row = self.db.one("SELECT experiment_id FROM trials WHERE id=?", [tid])
+                    exp_id = row["experiment_id"] if row else None
+            self.db.execute("INSERT OR REPLACE INTO checkpoints (uuid, trial_id, experiment_id, task_id, allocation_id,"
+                            " state, resources, metadata, steps_completed, report_time, searcher_metric) VALUES "
+                            "(?,?,?,?,?,?,?,?,?,?,?)",
+                            [body["uuid"], tid, exp_id, body.get("task_id"), body.get("allocation_id"), "COMPLETED",
+                             json.dumps(body.get("resources") or {}), json.dumps(body.get("metadata") or {}),
+                             steps, time.time(), metric])
+
+    def early_exit(self, tid: int, reason: str) -> None:
+        with self.lock:
+            exp, tr = self._trial(tid)
+            if tr.early_exit is not None:
+                raise ValueError("early exit already reported")
+            tr.early_exit = {"EXITED_REASON_INVALID_HP": "invalid_hp",
+                             "EXITED_REASON_USER_REQUESTED_STOP": "user_canceled"}.get(reason, "errored")
+            self._persist_trial(tr)
+
+    def preemption_signal(self, alloc_id: str, timeout: float) -> bool:
+        deadline = time.time() + timeout
+        with self.lock:
+            a = self.allocations.get(alloc_id)
+            if a is None:
+                return True
+            while not a.preempt and time.time() < deadline and not self._closed:
+                self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
+            return a.preempt
+
+    def ack_preemption(self, alloc_id: str) -> None:
+        with self.lock:
+            a = self.allocations.get(alloc_id)
+            if a is not None:
+                a.ack_preempt = True
+
+    def best_searcher_validation(self, eid: int) -> Optional[float]:
+        with self.lock:
+            exp = self._exp(eid)
+            sib = exp.config["searcher"].get("smaller_is_better", True)
+            row = self.db.one(f"SELECT {'MIN' if sib else 'MAX'}(best_validation) AS v FROM trials WHERE experiment_id=?",
+                              [eid])
+            return row["v"] if row else None
+
+    # ================================================================ logs
+    def add_logs(self, task_id: str, logs: List[Dict[str, Any]], allocation_id: Optional[str] = None) -> None:
+        with self.lock:
+            now = time.time()
+            self.db.conn.executemany(
+                "INSERT INTO task_logs (task_id, allocation_id, rank, ts, log) VALUES (?,?,?,?,?)",
+                [(task_id, allocation_id, l.get("rank"), now, l["log"]) for l in logs])
+            self.cv.notify_all()
+
+    def get_logs(self, task_id: str, after_id: int = 0, limit: int = 10000) -> List[Dict[str, Any]]:
+        return self.db.all("SELECT id, rank, ts, log FROM task_logs WHERE task_id=? AND id>? ORDER BY id LIMIT ?",
+                           [task_id, after_id, limit])
+
+    # ================================================================ custom searcher
+    def _custom_event(self, exp: ExperimentRec, ev: Dict[str, Any]) -> None:
+        if exp.searcher is not None:
+            return
+        exp.custom_event_id += 1
+        ev = dict(ev)
+        ev["id"] = exp.custom_event_id
+        exp.custom_events.append(ev)
+        self.cv.notify_all()
+
+    def get_searcher_events(self, eid: int, timeout: float = 0) -> List[Dict[str, Any]]:
+        deadline = time.time() + timeout
+        with self.lock:
+            exp = self._exp(eid)
+            while not exp.custom_events and time.time() < deadline and exp.state not in TERMINAL_EXP:
+                self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
+            return list(exp.custom_events)
+
+    def post_searcher_operations(self, eid: int, ops: List[Dict[str, Any]], triggered_by_event: int) -> None:
+        with self.lock:
+            exp = self._exp(eid)
+            exp.custom_events = [e for e in exp.custom_events if e["id"] > triggered_by_event]
+            self._process_ops(exp, ops)
+            self.cv.notify_all()
+
+    # ================================================================ checkpoint GC
+    def gc_experiment_checkpoints(self, eid: int, delete_all: bool = False) -> List[str]:
+        """Keep save_trial_latest / save_trial_best per trial and save_experiment_best overall
+        (reference ``master/internal/checkpoint_gc.go`` + ``exec/gc_checkpoints.py``)."""
+        from determined_amd import storage
+
+        with self.lock:
+            row = self.db.one("SELECT config FROM experiments WHERE id=?", [eid])
+            if row is None:
+                return []
+            cfg = row["config"]
+            cs = cfg["checkpoint_storage"]
+            sib = cfg["searcher"].get("smaller_is_better", True)
+            ckpts = self.db.all("SELECT uuid, trial_id, steps_completed, searcher_metric FROM checkpoints WHERE "
+                                "experiment_id=? AND state='COMPLETED'", [eid])
+            keep = set()
+            if not delete_all:
+                by_trial: Dict[int, List[Dict[str, Any]]] = {}
+                for c in ckpts:
+                    by_trial.setdefault(c["trial_id"], []).append(c)
+
+                def key(c: Dict[str, Any]) -> float:
+                    m = c["searcher_metric"]
+                    return float("inf") if m is None else (m if sib else -m)
+
+                for cs_list in by_trial.values():
+                    latest = sorted(cs_list, key=lambda c: -(c["steps_completed"] or 0))
+                    keep.update(c["uuid"] for c in latest[: int(cs.get("save_trial_latest", 1))])
+                    keep.update(c["uuid"] for c in sorted(cs_list, key=key)[: int(cs.get("save_trial_best", 1))]
+                                if c["searcher_metric"] is not None)
+                    # the latest checkpoint of a still-running trial is always kept (needed to resume)
+                keep.update(c["uuid"] for c in sorted(ckpts, key=key)[: int(cs.get("save_experiment_best", 0))]
+                            if c["searcher_metric"] is not None)
+                for tr in self.experiments.get(eid, ExperimentRec(eid, cfg, "")).trials.values():
+                    if tr.latest_checkpoint and tr.state not in TERMINAL_TRIAL:
+                        keep.add(tr.latest_checkpoint)
+            doomed = [c["uuid"] for c in ckpts if c["uuid"] not in keep]
+            if cfg.get("checkpoint_policy") == "none" and not delete_all:
+                doomed = [c["uuid"] for c in ckpts]
+        try:
+            sm = storage.build(cs)
+        except Exception as e:
+            logger.warning(f"checkpoint GC skipped: {e}")
+            return []
+        for u in doomed:
+            try:
+                sm.delete(u)
+            except Exception as e:
+                logger.warning(f"failed to delete checkpoint {u}: {e}")
+            self.db.update("checkpoints", "uuid", u, state="DELETED")
+        return doomed
+
+    def delete_checkpoints(self, uuids: List[str]) -> None:
+        from determined_amd import storage
+
+        for u in uuids:
+            row = self.db.one("SELECT c.uuid, e.config FROM checkpoints c LEFT JOIN experiments e "
+                              "ON c.experiment_id=e.id WHERE c.uuid=?", [u])
+            if row is None:
+                continue
+            if row.get("config"):
+                try:
+                    storage.build(row["config"]["checkpoint_storage"]).delete(u)
+                except Exception as e:
+                    logger.warning(f"delete {u}: {e}")
+            self.db.update("checkpoints", "uuid", u, state="DELETED")
+
+    # ================================================================ webhooks
+    def _fire_webhooks(self, exp: ExperimentRec, trigger: str, trial: Optional[TrialRec] = None) -> None:
+        hooks = self.db.all("SELECT * FROM webhooks")
+        if not hooks:
+            return
+        payload = {"event_type": trigger, "experiment": {"id": exp.id, "state": exp.state,
+                                                         "name": exp.config.get("name")}}
+        if trial is not None:
+            payload["trial"] = {"id": trial.id, "state": trial.state}
+
+        def send() -> None:
+            import requests
+
+            for h in hooks:
+                trig = h.get("triggers") or []
+                if trig and trigger not in [t.get("trigger_type", t) if isinstance(t, dict) else t for t in trig]:
+                    continue
+                try:
+                    requests.post(h["url"], json=payload, timeout=5)
+                except Exception as e:
+                    logger.debug(f"webhook {h['url']} failed: {e}")
+
+        threading.Thread(target=send, daemon=True).start()
+
+
+def _env_list(v: Any) -> List[str]:
+    if v is None:
+        return []
+    if isinstance(v, dict):
+        out: List[str] = []
+        for key in ("cpu", "gpu", "rocm"):
+            out += v.get(key) or []
+        return out
+    return list(v)
+
+
+def _isnum(v: Any) -> bool:
+    return isinstance(v, (int, float)) and not isinstance(v, bool)

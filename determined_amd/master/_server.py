@@ -1,0 +1,554 @@
+"""Master REST API (reference: ``master/internal/api_*.go`` behind grpc-gateway).
+
+JSON over HTTP on a threaded stdlib server; routes mirror the reference's ``/api/v1`` paths the
+harness and CLI use.  Long-polling endpoints (agent work, preemption signals, searcher events)
+block on the master's condition variable.
+"""
+
+import base64
+import json
+import logging
+import re
+import threading
+import time
+import urllib.parse
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from determined_amd import __version__
+from determined_amd.config import InvalidConfig
+from determined_amd.master._core import Master
+
+logger = logging.getLogger("determined_amd.master")
+
+Route = Tuple[str, "re.Pattern[str]", Callable[..., Any]]
+
+
+class HTTPError(Exception):
+    def __init__(self, status: int, message: str) -> None:
+        super().__init__(message)
+        self.status = status
+        self.message = message
+
+
+def _exp_summary(m: Master, row: Dict[str, Any]) -> Dict[str, Any]:
+    cfg = row.get("config") or {}
+    n = m.db.one("SELECT COUNT(*) AS n FROM trials WHERE experiment_id=?", [row["id"]])
+    return {
+        "id": row["id"], "name": row.get("name"), "state": row["state"], "archived": bool(row.get("archived")),
+        "progress": row.get("progress") or 0.0, "start_time": row.get("start_time"), "end_time": row.get("end_time"),
+        "description": row.get("description"), "labels": row.get("labels") or [], "owner": row.get("owner"),
+        "project": row.get("project"), "workspace": row.get("workspace"), "num_trials": n["n"] if n else 0,
+        "searcher_type": cfg.get("searcher", {}).get("name"), "parent_id": row.get("parent_id"),
+        "unmanaged": bool(row.get("unmanaged")),
+    }
+
+
+def _trial_summary(m: Master, t: Dict[str, Any]) -> Dict[str, Any]:
+    lv = m.db.one("SELECT steps_completed, metrics FROM metrics WHERE trial_id=? AND group_name='validation' "
+                  "ORDER BY id DESC LIMIT 1", [t["id"]])
+    lt = m.db.one("SELECT steps_completed, metrics FROM metrics WHERE trial_id=? AND group_name='training' "
+                  "ORDER BY id DESC LIMIT 1", [t["id"]])
+    return {
+        "id": t["id"], "experiment_id": t["experiment_id"], "request_id": t["request_id"], "state": t["state"],
+        "hparams": t["hparams"], "seed": t["seed"], "restarts": t["restarts"], "run_id": t["run_id"],
+        "start_time": t["start_time"], "end_time": t["end_time"], "latest_checkpoint": t["latest_checkpoint"],
+        "total_batches": t["total_batches"], "searcher_metric": t["searcher_metric"],
+        "best_validation": t["best_validation"], "runner_state": t.get("runner_state"),
+        "latest_validation": lv, "latest_training": lt, "task_id": f"trial-{t['id']}",
+    }
+
+
+def build_routes(m: Master) -> List[Route]:
+    routes: List[Route] = []
+
+    def route(method: str, pattern: str):
+        def deco(fn):
+            routes.append((method, re.compile("^" + pattern + "$"), fn))
+            return fn
+
+        return deco
+
+    # ---------------------------------------------------------------- master
+    @route("GET", "/api/v1/master")
+    def master_info(q, b):
+        return {"version": __version__, "cluster_id": m.cluster_id, "master_id": m.cluster_id,
+                "cluster_name": "determined_amd", "scheduler": m.policy,
+                "total_slots": m.sched.total_slots, "used_slots": m.sched.used_slots}
+
+    @route("GET", "/api/v1/me")
+    def me(q, b):
+        return {"user": {"username": "determined", "admin": True}}
+
+    @route("POST", "/api/v1/auth/login")
+    def login(q, b):
+        return {"token": m.auth_token or "", "user": {"username": b.get("username", "determined")}}
+
+    # ---------------------------------------------------------------- experiments
+    @route("POST", "/api/v1/experiments")
+    def create_exp(q, b):
+        md = base64.b64decode(b["model_def"]) if b.get("model_def") else None
+        try:
+            eid = m.create_experiment(b["config"], md, activate=b.get("activate", True),
+                                      parent_id=b.get("parent_id"), unmanaged=bool(b.get("unmanaged")))
+        except InvalidConfig as e:
+            raise HTTPError(400, str(e))
+        return {"experiment": _exp_summary(m, m.db.one("SELECT * FROM experiments WHERE id=?", [eid]))}
+
+    @route("GET", "/api/v1/experiments")
+    def list_exps(q, b):
+        rows = m.db.all("SELECT * FROM experiments WHERE state!='DELETED' ORDER BY id")
+        if q.get("archived") in ("false", "0"):
+            rows = [r for r in rows if not r["archived"]]
+        return {"experiments": [_exp_summary(m, r) for r in rows]}
+
+    @route("GET", r"/api/v1/experiments/(\d+)")
+    def get_exp(q, b, eid):
+        row = m.db.one("SELECT * FROM experiments WHERE id=?", [int(eid)])
+        if row is None:
+            raise HTTPError(404, f"experiment {eid} not found")
+        return {"experiment": _exp_summary(m, row), "config": row["config"]}
+
+    @route("GET", r"/api/v1/experiments/(\d+)/model_def")
+    def get_model_def(q, b, eid):
+        row = m.db.one("SELECT model_def FROM experiments WHERE id=?", [int(eid)])
+        if row is None:
+            raise HTTPError(404, "not found")
+        md = row["model_def"]
+        return {"b64_tgz": base64.b64encode(md).decode() if md else None}
+
+    for action, fn_name in (("pause", "pause_experiment"), ("activate", "activate_experiment"),
+                            ("kill", "kill_experiment"), ("cancel", "kill_experiment")):
+        def make(fn_name=fn_name):
+            def handler(q, b, eid):
+                getattr(m, fn_name)(int(eid))
+                return {}
+            return handler
+
+        routes.append(("POST", re.compile(rf"^/api/v1/experiments/(\d+)/{action}$"), make()))
+
+    @route("POST", r"/api/v1/experiments/(\d+)/archive")
+    def archive(q, b, eid):
+        m.archive_experiment(int(eid), True)
+        return {}
+
+    @route("POST", r"/api/v1/experiments/(\d+)/unarchive")
+    def unarchive(q, b, eid):
+        m.archive_experiment(int(eid), False)
+        return {}
+
+    @route("DELETE", r"/api/v1/experiments/(\d+)")
+    def delete_exp(q, b, eid):
+        try:
+            m.delete_experiment(int(eid))
+        except ValueError as e:
+            raise HTTPError(400, str(e))
+        return {}
+
+    @route("PATCH", r"/api/v1/experiments/(\d+)")
+    def patch_exp(q, b, eid):
+        cols = {k: v for k, v in b.items() if k in ("name", "description", "notes", "labels")}
+        m.db.update("experiments", "id", int(eid), **cols)
+        return {}
+
+    @route("GET", r"/api/v1/experiments/(\d+)/trials")
+    def exp_trials(q, b, eid):
+        rows = m.db.all("SELECT * FROM trials WHERE experiment_id=? ORDER BY id", [int(eid)])
+        return {"trials": [_trial_summary(m, t) for t in rows]}
+
+    @route("GET", r"/api/v1/experiments/(\d+)/checkpoints")
+    def exp_ckpts(q, b, eid):
+        rows = m.db.all("SELECT * FROM checkpoints WHERE experiment_id=? ORDER BY report_time", [int(eid)])
+        return {"checkpoints": rows}
+
+    @route("GET", r"/api/v1/experiments/(\d+)/searcher/best_searcher_validation_metric")
+    def best_val(q, b, eid):
+        v = m.best_searcher_validation(int(eid))
+        if v is None:
+            raise HTTPError(404, "no validations yet")
+        return {"metric": v}
+
+    @route("GET", r"/api/v1/experiments/(\d+)/searcher_events")
+    def searcher_events(q, b, eid):
+        return {"events": m.get_searcher_events(int(eid), float(q.get("timeout_seconds", 0)))}
+
+    @route("POST", r"/api/v1/experiments/(\d+)/searcher_operations")
+    def searcher_ops(q, b, eid):
+        m.post_searcher_operations(int(eid), b.get("operations", []), int(b.get("triggered_by_event", 0)))
+        return {}
+
+    @route("POST", r"/api/v1/experiments/(\d+)/gc")
+    def exp_gc(q, b, eid):
+        return {"deleted": m.gc_experiment_checkpoints(int(eid))}
+
+    # ---------------------------------------------------------------- trials
+    @route("GET", r"/api/v1/trials/(\d+)")
+    def get_trial(q, b, tid):
+        t = m.db.one("SELECT * FROM trials WHERE id=?", [int(tid)])
+        if t is None:
+            raise HTTPError(404, f"trial {tid} not found")
+        return {"trial": _trial_summary(m, t)}
+
+    @route("GET", r"/api/v1/trials/(\d+)/searcher/operation")
+    def trial_op(q, b, tid):
+        try:
+            return m.get_searcher_op(int(tid))
+        except KeyError as e:
+            raise HTTPError(404, str(e))
+
+    @route("POST", r"/api/v1/trials/(\d+)/searcher/completed_operation")
+    def trial_op_done(q, b, tid):
+        try:
+            m.complete_searcher_op(int(tid), int(b["op"]["length"]), b["searcher_metric"])
+        except ValueError as e:
+            raise HTTPError(400, str(e))
+        return {}
+
+    @route("POST", r"/api/v1/trials/(\d+)/progress")
+    def trial_progress(q, b, tid):
+        m.report_progress(int(tid), float(b.get("progress", 0.0)))
+        return {}
+
+    @route("POST", r"/api/v1/trials/(\d+)/metrics")
+    def trial_metrics(q, b, tid):
+        m.report_metrics(int(tid), b)
+        return {}
+
+    @route("GET", r"/api/v1/trials/(\d+)/metrics")
+    def get_trial_metrics(q, b, tid):
+        grp = q.get("group")
+        rows = m.db.all("SELECT group_name, steps_completed, metrics, trial_run_id, ts FROM metrics WHERE trial_id=? "
+                        + ("AND group_name=? " if grp else "") + "ORDER BY id", [int(tid)] + ([grp] if grp else []))
+        return {"metrics": rows}
+
+    @route("POST", r"/api/v1/trials/(\d+)/early_exit")
+    def trial_early_exit(q, b, tid):
+        try:
+            m.early_exit(int(tid), b.get("reason", ""))
+        except ValueError as e:
+            raise HTTPError(400, str(e))
+        return {}
+
+    @route("POST", r"/api/v1/trials/(\d+)/runner/metadata")
+    def trial_runner(q, b, tid):
+        m.db.update("trials", "id", int(tid), runner_state=b.get("state", ""))
+        return {}
+
+    @route("POST", r"/api/v1/trials/(\d+)/kill")
+    def trial_kill(q, b, tid):
+        with m.lock:
+            _, tr = m._trial(int(tid))
+            if tr.allocation is not None:
+                m._kill_allocation(tr.allocation)
+        return {}
+
+    @route("GET", r"/api/v1/trials/(\d+)/checkpoints")
+    def trial_ckpts(q, b, tid):
+        return {"checkpoints": m.db.all("SELECT * FROM checkpoints WHERE trial_id=? ORDER BY report_time", [int(tid)])}
+
+    # ---------------------------------------------------------------- checkpoints
+    @route("POST", "/api/v1/checkpoints")
+    def report_ckpt(q, b):
+        m.report_checkpoint(b)
+        return {}
+
+    @route("GET", r"/api/v1/checkpoints/([0-9a-f\-]+)")
+    def get_ckpt(q, b, u):
+        row = m.db.one("SELECT * FROM checkpoints WHERE uuid=?", [u])
+        if row is None:
+            raise HTTPError(404, f"checkpoint {u} not found")
+        exp = m.db.one("SELECT config FROM experiments WHERE id=?", [row["experiment_id"]]) \
+            if row.get("experiment_id") else None
+        row["checkpoint_storage"] = (exp or {}).get("config", {}).get("checkpoint_storage") if exp else None
+        return {"checkpoint": row}
+
+    @route("DELETE", r"/api/v1/checkpoints/([0-9a-f\-]+)")
+    def del_ckpt(q, b, u):
+        m.delete_checkpoints([u])
+        return {}
+
+    # ---------------------------------------------------------------- allocations
+    @route("GET", r"/api/v1/allocations/([^/]+)/signals/preemption")
+    def preempt(q, b, aid):
+        return {"preempt": m.preemption_signal(aid, float(q.get("timeout_seconds", 0)))}
+
+    @route("POST", r"/api/v1/allocations/([^/]+)/signals/ack_preemption")
+    def ack(q, b, aid):
+        m.ack_preemption(aid)
+        return {}
+
+    @route("GET", "/api/v1/allocations")
+    def allocs(q, b):
+        return {"allocations": [a.to_dict() for a in m.allocations.values() if a.state != "TERMINATED"]}
+
+    # ---------------------------------------------------------------- logs / tasks
+    @route("POST", "/api/v1/task/logs")
+    def post_logs(q, b):
+        m.add_logs(b["task_id"], b.get("logs", []), b.get("allocation_id"))
+        return {}
+
+    @route("GET", r"/api/v1/tasks/([^/]+)/logs")
+    def task_logs(q, b, task_id):
+        return {"logs": m.get_logs(task_id, int(q.get("after", 0)), int(q.get("limit", 10000)))}
+
+    @route("POST", "/api/v1/commands")
+    def create_cmd(q, b):
+        tid = m.create_command(b["command"], int(b.get("slots", 0)), b.get("env"), b.get("type", "COMMAND"),
+                               b.get("workdir_b64"))
+        return {"task_id": tid}
+
+    @route("GET", "/api/v1/tasks")
+    def list_tasks(q, b):
+        return {"tasks": m.db.all("SELECT * FROM tasks ORDER BY start_time")}
+
+    @route("GET", r"/api/v1/tasks/([^/]+)")
+    def get_task(q, b, task_id):
+        row = m.db.one("SELECT * FROM tasks WHERE id=?", [task_id])
+        if row is None:
+            raise HTTPError(404, f"task {task_id} not found")
+        return {"task": row}
+
+    @route("POST", r"/api/v1/tasks/([^/]+)/kill")
+    def kill_task(q, b, task_id):
+        m.kill_task(task_id)
+        return {}
+
+    # ---------------------------------------------------------------- agents
+    @route("POST", "/api/v1/agents/register")
+    def reg_agent(q, b):
+        return m.register_agent(b["agent_id"], int(b["slots"]), b.get("host", "127.0.0.1"), b.get("devices"),
+                                bool(b.get("gpu")), b.get("label", ""))
+
+    @route("GET", r"/api/v1/agents/([^/]+)/work")
+    def agent_work(q, b, agent_id):
+        try:
+            return {"commands": m.agent_poll(agent_id, float(q.get("timeout_seconds", 10)))}
+        except KeyError as e:
+            raise HTTPError(404, str(e))
+
+    @route("POST", r"/api/v1/agents/([^/]+)/events")
+    def agent_ev(q, b, agent_id):
+        m.agent_event(agent_id, b)
+        return {}
+
+    @route("GET", "/api/v1/agents")
+    def list_agents(q, b):
+        sa = m.sched.agents()
+        out = []
+        for aid, ag in m.agents.items():
+            owners = sa.get(aid, {}).get("slot_owner", [])
+            out.append({"id": aid, "host": ag["host"], "slots": ag["slots"], "devices": ag["devices"],
+                        "gpu": ag["gpu"], "enabled": ag["enabled"], "label": ag["label"],
+                        "slot_owner": owners, "used_slots": sum(1 for o in owners if o)})
+        return {"agents": out}
+
+    @route("POST", r"/api/v1/agents/([^/]+)/(enable|disable)")
+    def agent_enable(q, b, agent_id, what):
+        with m.lock:
+            if agent_id in m.agents:
+                m.agents[agent_id]["enabled"] = what == "enable"
+                m.sched.set_agent_enabled(agent_id, what == "enable")
+        return {}
+
+    @route("GET", "/api/v1/resource-pools")
+    def pools(q, b):
+        return {"resource_pools": [{"name": "default", "scheduler_type": m.policy, "slots_available": m.sched.total_slots,
+                                    "slots_used": m.sched.used_slots, "num_agents": len(m.agents)}]}
+
+    @route("GET", "/api/v1/job-queues")
+    def jobs(q, b):
+        return {"jobs": list(m.sched.requests().values())}
+
+    # ---------------------------------------------------------------- model registry
+    @route("POST", "/api/v1/models")
+    def create_model(q, b):
+        try:
+            mid = m.db.insert("models", name=b["name"], description=b.get("description", ""),
+                              metadata=b.get("metadata", {}), labels=b.get("labels", []), creation_time=time.time())
+        except Exception as e:
+            raise HTTPError(400, f"cannot create model: {e}")
+        return {"model": m.db.one("SELECT * FROM models WHERE id=?", [mid])}
+
+    @route("GET", "/api/v1/models")
+    def list_models(q, b):
+        return {"models": m.db.all("SELECT * FROM models ORDER BY id")}
+
+    @route("GET", r"/api/v1/models/([^/]+)")
+    def get_model(q, b, name):
+        name = urllib.parse.unquote(name)
+        row = m.db.one("SELECT * FROM models WHERE name=?", [name])
+        if row is None:
+            raise HTTPError(404, f"model {name} not found")
+        return {"model": row}
+
+    @route("PATCH", r"/api/v1/models/([^/]+)")
+    def patch_model(q, b, name):
+        cols = {k: v for k, v in b.items() if k in ("description", "metadata", "labels", "notes", "archived")}
+        m.db.update("models", "name", urllib.parse.unquote(name), **cols)
+        return {}
+
+    @route("DELETE", r"/api/v1/models/([^/]+)")
+    def del_model(q, b, name):
+        row = m.db.one("SELECT id FROM models WHERE name=?", [urllib.parse.unquote(name)])
+        if row:
+            m.db.execute("DELETE FROM model_versions WHERE model_id=?", [row["id"]])
+            m.db.execute("DELETE FROM models WHERE id=?", [row["id"]])
+        return {}
+
+    @route("POST", r"/api/v1/models/([^/]+)/versions")
+    def register_version(q, b, name):
+        name = urllib.parse.unquote(name)
+        row = m.db.one("SELECT id FROM models WHERE name=?", [name])
+        if row is None:
+            raise HTTPError(404, f"model {name} not found")
+        if m.db.one("SELECT uuid FROM checkpoints WHERE uuid=?", [b["checkpoint_uuid"]]) is None:
+            raise HTTPError(404, f"checkpoint {b['checkpoint_uuid']} not found")
+        last = m.db.one("SELECT MAX(version) AS v FROM model_versions WHERE model_id=?", [row["id"]])
+        ver = (last["v"] or 0) + 1
+        m.db.insert("model_versions", model_id=row["id"], version=ver, checkpoint_uuid=b["checkpoint_uuid"],
+                    name=b.get("name") or f"V{ver}", comment=b.get("comment", ""), metadata=b.get("metadata", {}),
+                    creation_time=time.time())
+        return {"model_version": m.db.one("SELECT * FROM model_versions WHERE model_id=? AND version=?",
+                                          [row["id"], ver])}
+
+    @route("GET", r"/api/v1/models/([^/]+)/versions")
+    def list_versions(q, b, name):
+        row = m.db.one("SELECT id FROM models WHERE name=?", [urllib.parse.unquote(name)])
+        if row is None:
+            raise HTTPError(404, "model not found")
+        return {"model_versions": m.db.all("SELECT * FROM model_versions WHERE model_id=? ORDER BY version",
+                                           [row["id"]])}
+
+    # ---------------------------------------------------------------- webhooks / templates
+    @route("POST", "/api/v1/webhooks")
+    def create_hook(q, b):
+        wid = m.db.insert("webhooks", url=b["url"], triggers=b.get("triggers", []),
+                          webhook_type=b.get("webhook_type", "DEFAULT"))
+        return {"webhook": m.db.one("SELECT * FROM webhooks WHERE id=?", [wid])}
+
+    @route("GET", "/api/v1/webhooks")
+    def list_hooks(q, b):
+        return {"webhooks": m.db.all("SELECT * FROM webhooks")}
+
+    @route("DELETE", r"/api/v1/webhooks/(\d+)")
+    def del_hook(q, b, wid):
+        m.db.execute("DELETE FROM webhooks WHERE id=?", [int(wid)])
+        return {}
+
+    @route("PUT", r"/api/v1/templates/([^/]+)")
+    def put_template(q, b, name):
+        m.db.execute("INSERT OR REPLACE INTO templates (name, config) VALUES (?,?)", [name, json.dumps(b["config"])])
+        return {}
+
+    @route("GET", "/api/v1/templates")
+    def list_templates(q, b):
+        return {"templates": m.db.all("SELECT * FROM templates")}
+
+    @route("GET", r"/api/v1/templates/([^/]+)")
+    def get_template(q, b, name):
+        row = m.db.one("SELECT * FROM templates WHERE name=?", [name])
+        if row is None:
+            raise HTTPError(404, f"template {name} not found")
+        return {"template": {"name": row["name"], "config": json.loads(row["config"])}}
+
+    @route("GET", "/metrics")
+    def prom(q, b):
+        exps = m.db.all("SELECT state, COUNT(*) AS n FROM experiments GROUP BY state")
+        lines = ["# TYPE det_slots_total gauge", f"det_slots_total {m.sched.total_slots}",
+                 "# TYPE det_slots_used gauge", f"det_slots_used {m.sched.used_slots}",
+                 "# TYPE det_experiments gauge"]
+        lines += [f'det_experiments{{state="{r["state"]}"}} {r["n"]}' for r in exps]
+        return _Raw("\n".join(lines) + "\n", "text/plain; version=0.0.4")
+
+    return routes
+
+
+class _Raw:
+    def __init__(self, body: str, ctype: str) -> None:
+        self.body = body
+        self.ctype = ctype
+
+
+class _Handler(BaseHTTPRequestHandler):
+    routes: List[Route] = []
+    master: Optional[Master] = None
+    protocol_version = "HTTP/1.1"
+
+    def log_message(self, fmt: str, *args: Any) -> None:
+        logger.debug("%s - " + fmt, self.address_string(), *args)
+
+    def _dispatch(self, method: str) -> None:
+        parsed = urllib.parse.urlparse(self.path)
+        q = {k: v[-1] for k, v in urllib.parse.parse_qs(parsed.query).items()}
+        n = int(self.headers.get("Content-Length") or 0)
+        raw = self.rfile.read(n) if n else b""
+        status, ctype = 200, "application/json"
+        try:
+            tok = self.master.auth_token if self.master else None
+            if tok and parsed.path.startswith("/api/") and not parsed.path.startswith("/api/v1/auth") and \
+                    self.headers.get("Authorization") != f"Bearer {tok}":
+                raise HTTPError(401, "unauthenticated")
+            body = json.loads(raw) if raw else {}
+            for meth, pat, fn in self.routes:
+                if meth != method:
+                    continue
+                mm = pat.match(parsed.path)
+                if mm:
+                    out = fn(q, body, *mm.groups())
+                    break
+            else:
+                raise HTTPError(404, f"no route {method} {parsed.path}")
+            if isinstance(out, _Raw):
+                data, ctype = out.body.encode(), out.ctype
+            else:
+                data = json.dumps(out, default=str).encode()
+        except HTTPError as e:
+            status, data = e.status, json.dumps({"error": e.message}).encode()
+        except KeyError as e:
+            status, data = 404, json.dumps({"error": str(e)}).encode()
+        except Exception as e:  # noqa: BLE001
+            logger.exception("request failed")
+            status, data = 500, json.dumps({"error": repr(e)}).encode()
+        self.send_response(status)
+        self.send_header("Content-Type", ctype)
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def do_GET(self) -> None:
+        self._dispatch("GET")
+
+    def do_POST(self) -> None:
+        self._dispatch("POST")
+
+    def do_DELETE(self) -> None:
+        self._dispatch("DELETE")
+
+    def do_PATCH(self) -> None:
+        self._dispatch("PATCH")
+
+    def do_PUT(self) -> None:
+        self._dispatch("PUT")
+
+
+class MasterServer:
+    def __init__(self, master: Master, host: str = "127.0.0.1", port: int = 8080) -> None:
+        handler = type("Handler", (_Handler,), {"routes": build_routes(master), "master": master})
+        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd.daemon_threads = True
+        self.master = master
+        self.port = self.httpd.server_address[1]
+        self.thread: Optional[threading.Thread] = None
+
+    def start(self) -> "MasterServer":
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="master-http")
+        self.thread.start()
+        return self
+
+    def serve_forever(self) -> None:
+        self.httpd.serve_forever()
+
+    def stop(self) -> None:
+        self.master.close()
+        self.httpd.shutdown()
+        self.httpd.server_close()
