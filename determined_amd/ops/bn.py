@@ -39,8 +39,15 @@ class _BNActFn(torch.autograd.Function):
 
 
 def _torch_bn_act(bn: nn.BatchNorm2d, x, residual, relu, momentum):
-    y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
-                     bn.training or not bn.track_running_stats, momentum, bn.eps)
+    if bn.running_mean is not None and bn.running_mean.dtype != x.dtype:
+        # low-precision activations with fp32 statistics: normalise in fp32
+        w = bn.weight.float() if bn.weight is not None else None
+        b = bn.bias.float() if bn.bias is not None else None
+        y = F.batch_norm(x.float(), bn.running_mean, bn.running_var, w, b,
+                         bn.training or not bn.track_running_stats, momentum, bn.eps).to(x.dtype)
+    else:
+        y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                         bn.training or not bn.track_running_stats, momentum, bn.eps)
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
