@@ -61,12 +61,31 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum, **kw)
         self.act = act
 
+    # num_batches_tracked is counted on the host (one tiny device add per BN layer per step is
+    # pure launch overhead: 53 launches/step in ResNet-50) and written into the buffer only when
+    # a state dict is produced.
+    _nbt_host: Optional[int] = None
+
+    def _nbt(self) -> int:
+        if self._nbt_host is None:
+            self._nbt_host = int(self.num_batches_tracked.item()) if self.num_batches_tracked is not None else 0
+        return self._nbt_host
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        if self.num_batches_tracked is not None and self._nbt_host is not None:
+            self.num_batches_tracked.fill_(self._nbt_host)
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        self._nbt_host = None
+
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
-            self.num_batches_tracked.add_(1)
+            self._nbt_host = self._nbt() + 1
             if self.momentum is None:
-                momentum = 1.0 / float(self.num_batches_tracked)
+                momentum = 1.0 / float(self._nbt_host)
         if not x.is_cuda or not self.affine:
             return _torch_bn_act(self, x, residual, self.act, momentum)
         from determined_amd import ops
