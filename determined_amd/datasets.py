@@ -49,3 +49,25 @@ class SyntheticImageNet(Dataset):
     def __getitem__(self, i: int):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
         return torch.randn(3, 224, 224, generator=g), int(torch.randint(0, 1000, (1,), generator=g))
+
+
+class SyntheticTokens(Dataset):
+    """Language-model samples of ``seq_len`` token ids: arithmetic progressions
+    ``(start + stride * j) mod V`` with a per-sample stride in [1, 16] and 10% random tokens.
+    Learnable (the model has to infer the stride from context), so the loss falls; generated
+    on the fly and vectorised, so it never bottlenecks a step."""
+
+    def __init__(self, n: int, seq_len: int, vocab_size: int, seed: int = 0, noise: float = 0.1) -> None:
+        self.n, self.seq_len, self.vocab, self.seed, self.noise = n, seq_len, vocab_size, seed, noise
+
+    def __len__(self) -> int:
+        return self.n
+
+    def __getitem__(self, i: int) -> torch.Tensor:
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
+        start = torch.randint(0, self.vocab, (1,), generator=g)
+        stride = torch.randint(1, 17, (1,), generator=g)
+        toks = (start + stride * torch.arange(self.seq_len)) % self.vocab
+        flip = torch.rand(self.seq_len, generator=g) < self.noise
+        toks[flip] = torch.randint(0, self.vocab, (int(flip.sum()),), generator=g)
+        return toks

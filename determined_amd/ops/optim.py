@@ -82,6 +82,8 @@ class _FusedBase(torch.optim.Optimizer):
         self._aux: Dict[torch.device, Dict[str, torch.Tensor]] = {}
         self.max_grad_norm: Optional[float] = None
         self.last_grad_norm: Optional[torch.Tensor] = None
+        # set by sharded engines (ZeRO): all-reduces the local sum of squared grads in place
+        self._partial_reducer: Optional[Callable[[torch.Tensor], None]] = None
 
     # -- step counter --------------------------------------------------------------------
     def _step_tensor(self, device: torch.device) -> torch.Tensor:
@@ -215,11 +217,16 @@ class _FusedBase(torch.optim.Optimizer):
                     e.l2norm_partial(pl.table, aux["partial"][off : off + pl.n_chunks], pl.g_dtype)
                     off += pl.n_chunks
                 fi = found_inf if found_inf is not None else aux["found_inf"]
-                # finalize also advances the device step counter unless overflow.
+                partial, n_partial = aux["partial"], total
+                if self._partial_reducer is not None:
+                    # sharded optimizer: combine this shard's sum of squares across ranks
+                    partial = aux["partial"][:total].sum(0, keepdim=True)
+                    self._partial_reducer(partial)
+                    n_partial = 1
                 # finalize: clip coefficient x inv loss scale, found_inf, and the device
                 # step counter (not advanced on overflow).
                 e.finalize(
-                    aux["partial"], total, inv_loss_scale, grad_scale, self.max_grad_norm or 0.0,
+                    partial, n_partial, inv_loss_scale, grad_scale, self.max_grad_norm or 0.0,
                     aux["out"], fi, step_t, True,
                 )
                 scale_t = aux["out"][0:1]
@@ -239,8 +246,13 @@ class _FusedBase(torch.optim.Optimizer):
             return
         gscale = inv_loss_scale * (float(grad_scale.item()) if grad_scale is not None else 1.0)
         params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
-        if self.max_grad_norm is not None and params:
-            norm = torch.sqrt(sum((p.grad.float() ** 2).sum() for p in params)) * gscale
+        if self.max_grad_norm is not None and (params or self._partial_reducer is not None):
+            sq = torch.zeros(1, dtype=torch.float32)
+            for p in params:
+                sq += (p.grad.float() ** 2).sum()
+            if self._partial_reducer is not None:
+                self._partial_reducer(sq)
+            norm = torch.sqrt(sq[0]) * gscale
             self.last_grad_norm = norm.reshape(1)
             if not torch.isfinite(norm):
                 return

@@ -100,7 +100,8 @@ class Trainer:
         else:
             if max_length is None and not test_mode:
                 raise ValueError("max_length is required for local training")
-        controller = _PyTorchTrialController(
+        controller_cls = getattr(self._trial, "trial_controller_class", None) or _PyTorchTrialController
+        controller = controller_cls(
             trial_inst=self._trial,
             context=self._context,
             checkpoint_period=checkpoint_period or Batch(0),
@@ -127,6 +128,17 @@ def init(*, hparams: Optional[Dict[str, Any]] = None, exp_conf: Optional[Dict[st
          distributed: Optional[core.DistributedContext] = None, aggregation_frequency: int = 1,
          enable_tensorboard_logging: bool = True, checkpoint_storage: Any = None,
          ddp_bucket_mb: float = 16.0) -> Iterator[PyTorchTrialContext]:
+    with _init_context(PyTorchTrialContext, hparams=hparams, exp_conf=exp_conf, distributed=distributed,
+                       aggregation_frequency=aggregation_frequency,
+                       enable_tensorboard_logging=enable_tensorboard_logging,
+                       checkpoint_storage=checkpoint_storage, ddp_bucket_mb=ddp_bucket_mb) as ctx:
+        yield ctx
+
+
+@contextlib.contextmanager
+def _init_context(context_cls: Any, *, hparams: Optional[Dict[str, Any]], exp_conf: Optional[Dict[str, Any]],
+                  distributed: Optional[core.DistributedContext], aggregation_frequency: int,
+                  enable_tensorboard_logging: bool, checkpoint_storage: Any, ddp_bucket_mb: float) -> Iterator[Any]:
     info = get_cluster_info()
     if distributed is None:
         distributed = _initialize_distributed_backend()
@@ -149,7 +161,7 @@ def init(*, hparams: Optional[Dict[str, Any]] = None, exp_conf: Optional[Dict[st
     _set_random_seeds(seed)
     num_gpus = 1 if torch.cuda.is_available() and slots > 0 else 0
     with core.init(distributed=distributed, checkpoint_storage=checkpoint_storage) as core_context:
-        ctx = PyTorchTrialContext(core_context=core_context, trial_seed=seed, hparams=hparams,
+        ctx = context_cls(core_context=core_context, trial_seed=seed, hparams=hparams,
                                   slots_per_trial=slots, num_gpus=num_gpus, exp_conf=exp_conf,
                                   aggregation_frequency=aggregation_frequency, steps_completed=steps_completed,
                                   managed_training=managed, debug_enabled=False,

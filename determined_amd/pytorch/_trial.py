@@ -244,6 +244,19 @@ class _PyTorchTrialController:
             self.validation_loader = vl
             self._val_shard = (1, 0)
 
+    def _make_training_enumerator(self) -> Iterator:
+        """Yields ``(batch_idx, batch)`` pairs for ``_train_with_boundaries``."""
+        return enumerate(iter(self.training_loader), start=self.state.batches_trained)
+
+    def _iter_eval_metrics(self) -> Iterator[Dict[str, Any]]:
+        """Runs ``evaluate_batch`` over this rank's share of the validation data."""
+        n_shards, shard = self._val_shard
+        for idx, batch in enumerate(self.validation_loader):
+            if idx % n_shards != shard:
+                continue
+            batch = self.context.to_device(batch)
+            yield self.trial.evaluate_batch(batch=batch, batch_idx=idx)
+
     # -- checkpointing -----------------------------------------------------------------------
     def _save(self, path: pathlib.Path) -> None:
         path.mkdir(parents=True, exist_ok=True)
@@ -506,15 +519,12 @@ class _PyTorchTrialController:
         self.context.reset_reducers()
         dist = self.context.distributed
         if self._evaluate_batch_defined():
-            n_shards, shard = self._val_shard
             sums: Dict[str, List[Any]] = {}
             num = 0
             outputs = []
-            for idx, batch in enumerate(self.validation_loader):
-                if idx % n_shards != shard:
-                    continue
-                batch = self.context.to_device(batch)
-                vm = self.trial.evaluate_batch(batch=batch, batch_idx=idx)
+            for vm in self._iter_eval_metrics():
+                if not isinstance(vm, dict):
+                    raise TypeError("evaluate_batch must return a dict of metric names to values")
                 outputs.append(vm)
                 for k, v in vm.items():
                     sums.setdefault(k, []).append(v.detach() if isinstance(v, torch.Tensor) else v)
@@ -594,7 +604,7 @@ class _PyTorchTrialController:
                 with self.core_context.checkpoint.restore_path(self.latest_checkpoint) as p:
                     self._load(pathlib.Path(p))
             self._set_data_loaders()
-            self.training_enumerator = enumerate(iter(self.training_loader), start=self.state.batches_trained)
+            self.training_enumerator = self._make_training_enumerator()
             for cb in self.callbacks.values():
                 cb.on_training_start()
             if self.profiling_enabled:
