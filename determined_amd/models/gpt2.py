@@ -150,7 +150,8 @@ class GPT2LMHeadModel(nn.Module):
 
 def lm_loss(logits: torch.Tensor, labels: torch.Tensor, vocab_size: int) -> torch.Tensor:
     """Shifted next-token cross-entropy in fp32 (``-100`` labels ignored, padded vocab masked)."""
-    lg = logits[:, :-1, :vocab_size].reshape(-1, vocab_size).float()
+    lg = logits[:, :-1, :vocab_size].reshape(-1, vocab_size)
+    lg = lg.to(torch.promote_types(lg.dtype, torch.float32))
     return F.cross_entropy(lg, labels[:, 1:].reshape(-1), ignore_index=-100)
 
 

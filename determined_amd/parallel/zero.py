@@ -683,6 +683,8 @@ class ZeroEngine(nn.Module):
                     else:
                         gv = sp.G.narrow(0, b.start + boff, e - s)
                     frag = nn.Parameter(pv, requires_grad=False)
+                    if gv.dtype != pv.dtype and hasattr(frag, "grad_dtype"):
+                        frag.grad_dtype = None  # fp32-accumulated grads on bf16 weights
                     frag.grad = gv
                     gi = self._group_of[id(p)]
                     frag_groups[gi].append(frag)
