@@ -81,14 +81,17 @@ class CheckpointContext:
             return storage_id
         storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
         resources: Dict[str, int] = {}
+        self._dist.allgather_local(None)  # every local rank finished writing before anyone lists
         if ckpt_dir is not None:
             resources = storage.list_directory(ckpt_dir)
             if selector is not None:
                 resources = {k: v for k, v in resources.items() if selector(k)}
-            # local workers sharing one directory upload only once (lowest local rank)
-            owners = self._dist.allgather_local(str(pathlib.Path(ckpt_dir).resolve()))
-            if selector is None and owners.index(str(pathlib.Path(ckpt_dir).resolve())) != self._dist.local_rank:
-                resources = {}
+            # local workers sharing one directory upload each file once (lowest local rank that has it)
+            key = str(pathlib.Path(ckpt_dir).resolve())
+            local = [(d, set(fs)) for d, fs in self._dist.allgather_local((key, sorted(resources)))]
+            me = self._dist.local_rank
+            resources = {f: n for f, n in resources.items()
+                         if next(i for i, (d, fs) in enumerate(local) if d == key and f in fs) == me}
             if resources:
                 self._storage_manager.upload(src=ckpt_dir, dst=storage_id, paths=sorted(resources))
         merged_md, merged_res = self._merge(metadata, resources)
