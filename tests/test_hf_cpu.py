@@ -59,3 +59,51 @@ def test_hf_trainer_detcallback_local(monkeypatch):
         files = {str(f.relative_to(c)) for c in ckpts for f in c.rglob("*") if f.is_file()}
         assert any(f.startswith("checkpoint-6/") for f in files)
         assert any(f.endswith("my_data.json") for f in files)
+
+
+def test_model_hub_base_transformer_trial_local():
+    from torch.utils.data import Dataset
+
+    from determined_amd import pytorch
+    from determined_amd.model_hub import huggingface as mh
+    from determined_amd.model_hub.utils import expand_like
+
+    mod = _load_run_mlm()
+
+    class DS(Dataset):
+        def __init__(self, n):
+            self.d = mod.SyntheticMLM(n, 16, 2000)
+
+        def __len__(self):
+            return len(self.d)
+
+        def __getitem__(self, i):
+            return self.d[i]
+
+    class MLMTrial(mh.BaseTransformerTrial):
+        def build_training_data_loader(self):
+            return pytorch.DataLoader(DS(64), batch_size=self.context.get_per_slot_batch_size())
+
+        def build_validation_data_loader(self):
+            return pytorch.DataLoader(DS(8), batch_size=4)
+
+        def evaluate_batch(self, batch, batch_idx):
+            return {"validation_loss": self.model(**batch)["loss"]}
+
+    hp = {"model_mode": "masked-lm", "model_name": "none", "model_type": "bert",
+          "config_overrides": {"hidden_size": 32, "num_hidden_layers": 1, "num_attention_heads": 2,
+                               "intermediate_size": 64, "vocab_size": 2000},
+          "use_pretrained_weights": False, "global_batch_size": 8, "learning_rate": 1e-3, "num_training_steps": 4,
+          "max_grad_norm": 1.0}
+    cfg, tok, model = mh.default_parse_config_tokenizer_model_kwargs(hp)
+    assert cfg.model_type == "bert" and tok.pretrained_model_name_or_path == "none"
+    with tempfile.TemporaryDirectory() as d:
+        with pytorch.init(hparams=hp, exp_conf={"data": {}, "searcher": {"max_length": {"batches": 4}}},
+                          checkpoint_storage=d) as ctx:
+            trial = MLMTrial(ctx)  # model_type -> AutoConfig.for_model: offline random init
+            assert trial.config.hidden_size == 32 and trial.optimizer.max_grad_norm == 1.0
+            pytorch.Trainer(trial, ctx).fit(max_length=pytorch.Batch(4), validation_period=pytorch.Batch(4))
+    import numpy as np
+
+    out = expand_like([np.ones((2, 3)), np.ones((1, 5))])
+    assert out.shape == (3, 5) and out[2, 4] == 1 and out[0, 4] == -100
