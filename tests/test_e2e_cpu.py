@@ -1,0 +1,157 @@
+"""Cluster end to end on CPU: in-process master + agent (2 CPU slots) running real trial
+processes (``exec.harness`` under the agent).  Covers experiment lifecycle, searchers,
+restarts, InvalidHP, checkpoints/GC, logs, model registry and the ``det`` CLI."""
+
+import base64
+import contextlib
+import io
+import json
+import os
+import pathlib
+import tempfile
+import threading
+import time
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+TINY = ROOT / "tests" / "fixtures" / "tiny_trial"
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    from determined_amd.agent import Agent
+    from determined_amd.common.api import Session
+    from determined_amd.master import start_master
+
+    srv = start_master()
+    url = f"http://127.0.0.1:{srv.port}"
+    work = tempfile.mkdtemp()
+    ag = Agent(url, "e2e-agent", slots=2, work_root=work)
+    th = threading.Thread(target=ag.run, daemon=True)
+    th.start()
+    ck = tempfile.mkdtemp()
+    yield {"url": url, "session": Session(url), "ckpt": ck, "master": srv}
+    if hasattr(ag, "stop"):
+        ag.stop()
+    srv.stop() if hasattr(srv, "stop") else None
+
+
+def _create(cl, cfg, model_dir=TINY, activate=True):
+    from determined_amd.cli import tar_model_dir
+
+    cfg = dict(cfg)
+    cfg.setdefault("checkpoint_storage", {"type": "shared_fs", "host_path": cl["ckpt"]})
+    cfg.setdefault("entrypoint", "model_def:TinyTrial")
+    r = cl["session"].post("/api/v1/experiments", {"config": cfg, "activate": activate,
+                                                   "model_def": base64.b64encode(tar_model_dir(str(model_dir))).decode()})
+    return r["experiment"]["id"]
+
+
+def _wait(cl, eid, states=("COMPLETED", "ERROR", "CANCELED"), timeout=240):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        e = cl["session"].get(f"/api/v1/experiments/{eid}")["experiment"]
+        if e["state"] in states:
+            return e
+        time.sleep(0.5)
+    raise TimeoutError(f"experiment {eid} stuck in {e['state']}")
+
+
+def _trials(cl, eid):
+    return cl["session"].get(f"/api/v1/experiments/{eid}/trials")["trials"]
+
+
+HP = {"lr": 0.1, "global_batch_size": 16}
+
+
+def test_single_trial(cluster):
+    eid = _create(cluster, {"name": "single", "hyperparameters": HP,
+                            "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": 12}},
+                            "min_validation_period": {"batches": 6}})
+    e = _wait(cluster, eid)
+    assert e["state"] == "COMPLETED"
+    (t,) = _trials(cluster, eid)
+    assert t["state"] == "COMPLETED" and t["total_batches"] == 12
+    s = cluster["session"]
+    ms = s.get(f"/api/v1/trials/{t['id']}/metrics")
+    text = json.dumps(ms)
+    assert "validation_loss" in text and "loss" in text
+    cks = s.get(f"/api/v1/experiments/{eid}/checkpoints")["checkpoints"]
+    assert cks and all(os.path.isdir(os.path.join(cluster["ckpt"], c["uuid"])) for c in cks)
+    logs = s.get(f"/api/v1/tasks/trial-{t['id']}/logs")["logs"]
+    assert any("rank" in l["log"] or "INFO" in l["log"] for l in logs)
+
+
+def test_adaptive_asha(cluster):
+    eid = _create(cluster, {
+        "name": "asha",
+        "hyperparameters": {"global_batch_size": 16, "lr": {"type": "log", "minval": -3, "maxval": 0, "base": 10}},
+        "searcher": {"name": "adaptive_asha", "metric": "validation_loss", "max_length": {"batches": 16},
+                     "max_trials": 4, "max_rungs": 2, "divisor": 4, "mode": "aggressive", "max_concurrent_trials": 2}})
+    e = _wait(cluster, eid)
+    assert e["state"] == "COMPLETED"
+    ts = _trials(cluster, eid)
+    assert len(ts) == 4 and all(t["state"] == "COMPLETED" for t in ts)
+    lengths = sorted(t["total_batches"] for t in ts)
+    assert lengths[-1] == 16 and lengths[0] < 16  # promoted vs stopped at the lower rung
+
+
+def test_restart_and_invalid_hp(cluster):
+    marker = os.path.join(tempfile.mkdtemp(), "crashed")
+    eid = _create(cluster, {"name": "flaky", "max_restarts": 2,
+                            "hyperparameters": {**HP, "crash_marker": marker},
+                            "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": 6}}})
+    e = _wait(cluster, eid)
+    (t,) = _trials(cluster, eid)
+    assert e["state"] == "COMPLETED" and t["restarts"] == 1 and os.path.exists(marker)
+    eid2 = _create(cluster, {"name": "invalid", "hyperparameters": {**HP, "invalid": True},
+                             "searcher": {"name": "single", "metric": "validation_loss",
+                                          "max_length": {"batches": 6}}})
+    e2 = _wait(cluster, eid2)
+    (t2,) = _trials(cluster, eid2)
+    assert e2["state"] == "COMPLETED" and t2["restarts"] == 0 and t2["total_batches"] == 0
+
+
+def test_pause_activate_and_kill(cluster):
+    s = cluster["session"]
+    eid = _create(cluster, {"name": "paused", "hyperparameters": HP,
+                            "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": 6}}},
+                  activate=False)
+    time.sleep(1.5)
+    assert s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"] == "PAUSED"
+    assert _trials(cluster, eid)[0]["total_batches"] == 0
+    s.post(f"/api/v1/experiments/{eid}/activate", {})
+    assert _wait(cluster, eid)["state"] == "COMPLETED"
+    eid2 = _create(cluster, {"name": "killed", "hyperparameters": HP,
+                             "searcher": {"name": "single", "metric": "validation_loss",
+                                          "max_length": {"batches": 100000}}})
+    time.sleep(2)
+    s.post(f"/api/v1/experiments/{eid2}/kill", {})
+    assert _wait(cluster, eid2)["state"] == "CANCELED"
+
+
+def test_grid_and_model_registry_and_cli(cluster):
+    from determined_amd.cli import main as det
+
+    eid = _create(cluster, {"name": "grid",
+                            "hyperparameters": {"global_batch_size": 16,
+                                                "lr": {"type": "categorical", "vals": [0.01, 0.1]}},
+                            "searcher": {"name": "grid", "metric": "validation_loss", "max_length": {"batches": 4}}})
+    assert _wait(cluster, eid)["state"] == "COMPLETED"
+    ts = _trials(cluster, eid)
+    assert sorted(t["hparams"]["lr"] for t in ts) == [0.01, 0.1]
+    s = cluster["session"]
+    ck = s.get(f"/api/v1/experiments/{eid}/checkpoints")["checkpoints"][0]["uuid"]
+    s.post("/api/v1/models", {"name": "tiny-model", "description": "e2e"})
+    s.post("/api/v1/models/tiny-model/versions", {"checkpoint_uuid": ck})
+    vs = s.get("/api/v1/models/tiny-model/versions")
+    assert json.dumps(vs).count(ck) >= 1
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = det(["-m", cluster["url"], "experiment", "list"])
+    assert rc in (0, None) and "grid" in out.getvalue()
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        det(["-m", cluster["url"], "agent", "list"])
+    assert "e2e-agent" in out.getvalue()
