@@ -1,0 +1,657 @@
+"""Python SDK for the master (reference: ``harness/determined/experimental/client.py`` and
+``common/experimental/{experiment,trial,checkpoint,model}.py``).
+
+.. code-block:: python
+
+    from determined_amd.experimental import client
+    client.login("http://127.0.0.1:8080")
+    exp = client.create_experiment("const.yaml", "examples/mnist_pytorch")
+    exp.wait()
+    ckpt = exp.top_checkpoint()
+    path = ckpt.download()
+    model = client.create_model("mnist")
+    model.register_version(ckpt.uuid)
+
+Objects are thin views over REST responses (``reload()`` refreshes them).  Checkpoint
+download reads the experiment's ``checkpoint_storage`` directly (shared_fs / directory) like
+the reference's ``DownloadMode.DIRECT``, falling back to nothing else since there is no
+master-proxied download in this build.
+"""
+
+import base64
+import enum
+import io
+import json
+import os
+import pathlib
+import tarfile
+import time
+from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Set, Union
+
+import yaml
+
+from determined_amd.common.api import NotFoundException, Session
+
+_session: Optional[Session] = None
+
+
+def login(master: Optional[str] = None, user: Optional[str] = None, password: Optional[str] = None,
+          token: Optional[str] = None) -> Session:
+    """Set the module-level session (``DET_MASTER`` or ``http://127.0.0.1:8080`` by default)."""
+    global _session
+    url = master or os.environ.get("DET_MASTER") or "http://127.0.0.1:8080"
+    s = Session(url, token=token)
+    if user is not None and token is None:
+        r = s.post("/api/v1/auth/login", {"username": user, "password": password or ""})
+        s.token = (r or {}).get("token") or None
+    _session = s
+    return s
+
+
+def logout() -> None:
+    global _session
+    _session = None
+
+
+def _s() -> Session:
+    if _session is None:
+        login()
+    assert _session is not None
+    return _session
+
+
+class ExperimentState(enum.Enum):
+    ACTIVE = "ACTIVE"
+    PAUSED = "PAUSED"
+    STOPPING_COMPLETED = "STOPPING_COMPLETED"
+    STOPPING_CANCELED = "STOPPING_CANCELED"
+    STOPPING_ERROR = "STOPPING_ERROR"
+    COMPLETED = "COMPLETED"
+    CANCELED = "CANCELED"
+    ERROR = "ERROR"
+    DELETED = "DELETED"
+
+
+TERMINAL = {ExperimentState.COMPLETED, ExperimentState.CANCELED, ExperimentState.ERROR, ExperimentState.DELETED}
+
+
+class TrialState(enum.Enum):
+    ACTIVE = "ACTIVE"
+    PAUSED = "PAUSED"
+    COMPLETED = "COMPLETED"
+    CANCELED = "CANCELED"
+    ERROR = "ERROR"
+
+
+class CheckpointState(enum.Enum):
+    ACTIVE = "ACTIVE"
+    COMPLETED = "COMPLETED"
+    DELETED = "DELETED"
+    PARTIALLY_DELETED = "PARTIALLY_DELETED"
+    ERROR = "ERROR"
+
+
+class DownloadMode(enum.Enum):
+    AUTO = "auto"
+    DIRECT = "direct"
+    MASTER = "master"
+
+
+def _tar_dir(path: str) -> bytes:
+    from determined_amd.cli import tar_model_dir
+
+    return tar_model_dir(path)
+
+
+# ---------------------------------------------------------------------------------------------
+# checkpoints
+# ---------------------------------------------------------------------------------------------
+class Checkpoint:
+    def __init__(self, session: Session, uuid: str, data: Optional[Dict[str, Any]] = None) -> None:
+        self._session = session
+        self.uuid = uuid
+        self._data = data or {}
+        if not data:
+            self.reload()
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/checkpoints/{self.uuid}")["checkpoint"]
+
+    @property
+    def metadata(self) -> Dict[str, Any]:
+        return dict(self._data.get("metadata") or {})
+
+    @property
+    def state(self) -> CheckpointState:
+        return CheckpointState(self._data.get("state") or "COMPLETED")
+
+    @property
+    def trial_id(self) -> Optional[int]:
+        return self._data.get("trial_id")
+
+    @property
+    def steps_completed(self) -> Optional[int]:
+        return self._data.get("steps_completed")
+
+    @property
+    def resources(self) -> Dict[str, int]:
+        return dict(self._data.get("resources") or {})
+
+    @property
+    def searcher_metric(self) -> Optional[float]:
+        return self._data.get("searcher_metric")
+
+    def _storage(self) -> Any:
+        from determined_amd import storage
+
+        cfg = self._data.get("checkpoint_storage")
+        if cfg is None:
+            self.reload()
+            cfg = self._data.get("checkpoint_storage")
+        if cfg is None:
+            raise RuntimeError(f"checkpoint {self.uuid} has no experiment storage configuration")
+        return storage.build(cfg)
+
+    def download(self, path: Optional[str] = None, mode: DownloadMode = DownloadMode.AUTO) -> str:
+        if mode == DownloadMode.MASTER:
+            raise NotImplementedError("master-proxied checkpoint download is not supported; use DIRECT")
+        path = path or os.path.join("checkpoints", self.uuid)
+        os.makedirs(path, exist_ok=True)
+        self._storage().download(src=self.uuid, dst=path)
+        self.write_metadata_file(os.path.join(path, "metadata.json"))
+        return path
+
+    def write_metadata_file(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump(self.metadata, f, indent=2, sort_keys=True)
+
+    def add_metadata(self, metadata: Dict[str, Any]) -> None:
+        md = self.metadata
+        md.update(metadata)
+        self._session.patch(f"/api/v1/checkpoints/{self.uuid}", {"metadata": md})
+        self._data["metadata"] = md
+
+    def remove_metadata(self, keys: List[str]) -> None:
+        md = {k: v for k, v in self.metadata.items() if k not in keys}
+        self._session.patch(f"/api/v1/checkpoints/{self.uuid}", {"metadata": md})
+        self._data["metadata"] = md
+
+    def delete(self) -> None:
+        self._session.delete(f"/api/v1/checkpoints/{self.uuid}")
+
+    def get_metrics(self, group: Optional[str] = None) -> Iterable[Dict[str, Any]]:
+        if self.trial_id is None:
+            return []
+        steps = self.steps_completed
+        return [m for m in Trial(self._session, self.trial_id).iter_metrics(group or "validation")
+                if m["steps_completed"] == steps]
+
+    def __repr__(self) -> str:
+        return f"Checkpoint(uuid={self.uuid})"
+
+
+# ---------------------------------------------------------------------------------------------
+# trials
+# ---------------------------------------------------------------------------------------------
+class Trial:
+    def __init__(self, session: Session, trial_id: int, data: Optional[Dict[str, Any]] = None) -> None:
+        self._session = session
+        self.id = trial_id
+        self._data = data or {}
+        if not data:
+            self.reload()
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/trials/{self.id}")["trial"]
+
+    @property
+    def experiment_id(self) -> int:
+        return int(self._data["experiment_id"])
+
+    @property
+    def hparams(self) -> Dict[str, Any]:
+        return dict(self._data.get("hparams") or {})
+
+    @property
+    def state(self) -> TrialState:
+        return TrialState(self._data["state"])
+
+    @property
+    def summary_metrics(self) -> Dict[str, Any]:
+        return {"latest_validation": self._data.get("latest_validation"),
+                "latest_training": self._data.get("latest_training")}
+
+    def iter_logs(self, follow: bool = False, head: Optional[int] = None, tail: Optional[int] = None,
+                  search_text: Optional[str] = None) -> Iterator[str]:
+        after = 0
+        emitted: List[str] = []
+        while True:
+            rows = self._session.get(f"/api/v1/tasks/trial-{self.id}/logs", params={"after": after})["logs"]
+            for r in rows:
+                after = max(after, int(r["id"]))
+                if search_text and search_text not in r["log"]:
+                    continue
+                emitted.append(r["log"])
+                if tail is None:
+                    yield r["log"]
+                    if head is not None and len(emitted) >= head:
+                        return
+            if not follow:
+                break
+            self.reload()
+            if self._data["state"] in ("COMPLETED", "CANCELED", "ERROR") and not rows:
+                break
+            time.sleep(0.5)
+        if tail is not None:
+            yield from emitted[-tail:]
+
+    def logs(self, *args: Any, **kwargs: Any) -> Iterable[str]:
+        return self.iter_logs(*args, **kwargs)
+
+    def kill(self) -> None:
+        self._session.post(f"/api/v1/trials/{self.id}/kill", {})
+
+    def list_checkpoints(self) -> List[Checkpoint]:
+        rows = self._session.get(f"/api/v1/trials/{self.id}/checkpoints")["checkpoints"]
+        return [Checkpoint(self._session, r["uuid"], r) for r in rows]
+
+    def top_checkpoint(self, sort_by: Optional[str] = None, smaller_is_better: Optional[bool] = None) -> Checkpoint:
+        cks = self.list_checkpoints()
+        if not cks:
+            raise RuntimeError(f"trial {self.id} has no checkpoints")
+        return _best(cks, self._session, self.experiment_id, sort_by, smaller_is_better)[0]
+
+    def select_checkpoint(self, latest: bool = False, best: bool = False, uuid: Optional[str] = None,
+                          sort_by: Optional[str] = None, smaller_is_better: Optional[bool] = None) -> Checkpoint:
+        if sum([latest, best, uuid is not None]) != 1:
+            raise ValueError("pass exactly one of latest / best / uuid")
+        if uuid is not None:
+            return Checkpoint(self._session, uuid)
+        if latest:
+            cks = self.list_checkpoints()
+            return max(cks, key=lambda c: c.steps_completed or 0)
+        return self.top_checkpoint(sort_by, smaller_is_better)
+
+    def iter_metrics(self, group: str) -> Iterator[Dict[str, Any]]:
+        rows = self._session.get(f"/api/v1/trials/{self.id}/metrics", params={"group": group})["metrics"]
+        for r in rows:
+            yield {"trial_id": self.id, "steps_completed": r["steps_completed"], "metrics": r["metrics"],
+                   "group": r["group_name"], "trial_run_id": r.get("trial_run_id"), "time": r.get("ts")}
+
+    def stream_training_metrics(self) -> Iterable[Dict[str, Any]]:
+        return self.iter_metrics("training")
+
+    def stream_validation_metrics(self) -> Iterable[Dict[str, Any]]:
+        return self.iter_metrics("validation")
+
+    def __repr__(self) -> str:
+        return f"Trial(id={self.id})"
+
+
+def _best(cks: List[Checkpoint], session: Session, exp_id: int, sort_by: Optional[str],
+          smaller_is_better: Optional[bool]) -> List[Checkpoint]:
+    cfg = session.get(f"/api/v1/experiments/{exp_id}")["config"]
+    metric = sort_by or cfg["searcher"]["metric"]
+    sib = cfg["searcher"].get("smaller_is_better", True) if smaller_is_better is None else smaller_is_better
+
+    def val(c: Checkpoint) -> float:
+        v = c.searcher_metric if sort_by is None else None
+        if v is None:
+            for mrow in Trial(session, c.trial_id).iter_metrics("validation") if c.trial_id else []:
+                if mrow["steps_completed"] == c.steps_completed and metric in (mrow["metrics"] or {}):
+                    v = mrow["metrics"][metric]
+        if v is None:
+            return float("inf") if sib else float("-inf")
+        return float(v)
+
+    return sorted(cks, key=val, reverse=not sib)
+
+
+# ---------------------------------------------------------------------------------------------
+# experiments
+# ---------------------------------------------------------------------------------------------
+class Experiment:
+    def __init__(self, session: Session, experiment_id: int, data: Optional[Dict[str, Any]] = None) -> None:
+        self._session = session
+        self._id = experiment_id
+        self._data = data or {}
+        self._config: Optional[Dict[str, Any]] = None
+        if not data:
+            self.reload()
+
+    @property
+    def id(self) -> int:
+        return self._id
+
+    def reload(self) -> None:
+        r = self._session.get(f"/api/v1/experiments/{self._id}")
+        self._data, self._config = r["experiment"], r.get("config")
+
+    @property
+    def state(self) -> ExperimentState:
+        return ExperimentState(self._data["state"])
+
+    @property
+    def name(self) -> str:
+        return self._data.get("name") or ""
+
+    @property
+    def config(self) -> Dict[str, Any]:
+        if self._config is None:
+            self.reload()
+        return dict(self._config or {})
+
+    @property
+    def progress(self) -> float:
+        return float(self._data.get("progress") or 0.0)
+
+    @property
+    def labels(self) -> Set[str]:
+        return set(self._data.get("labels") or [])
+
+    def _patch(self, **cols: Any) -> None:
+        self._session.patch(f"/api/v1/experiments/{self._id}", cols)
+        self._data.update(cols)
+
+    def set_name(self, name: str) -> None:
+        self._patch(name=name)
+
+    def set_description(self, description: str) -> None:
+        self._patch(description=description)
+
+    def set_notes(self, notes: str) -> None:
+        self._patch(notes=notes)
+
+    def add_label(self, label: str) -> None:
+        self.set_labels(self.labels | {label})
+
+    def remove_label(self, label: str) -> None:
+        self.set_labels(self.labels - {label})
+
+    def set_labels(self, labels: Set[str]) -> None:
+        self._patch(labels=sorted(labels))
+
+    def _action(self, verb: str) -> None:
+        self._session.post(f"/api/v1/experiments/{self._id}/{verb}", {})
+
+    def activate(self) -> None:
+        self._action("activate")
+
+    def pause(self) -> None:
+        self._action("pause")
+
+    def kill(self) -> None:
+        self._action("kill")
+
+    def cancel(self) -> None:
+        self._action("cancel")
+
+    def archive(self) -> None:
+        self._action("archive")
+
+    def unarchive(self) -> None:
+        self._action("unarchive")
+
+    def delete(self) -> None:
+        self._session.delete(f"/api/v1/experiments/{self._id}")
+
+    def download_code(self, output_dir: Optional[str] = None) -> str:
+        b64 = self._session.get(f"/api/v1/experiments/{self._id}/model_def")["b64_tgz"]
+        out = output_dir or f"exp-{self._id}-code"
+        os.makedirs(out, exist_ok=True)
+        if b64:
+            with tarfile.open(fileobj=io.BytesIO(base64.b64decode(b64)), mode="r:gz") as tf:
+                tf.extractall(out, filter="data") if hasattr(tarfile, "data_filter") else tf.extractall(out)
+        return out
+
+    def list_trials(self) -> List[Trial]:
+        rows = self._session.get(f"/api/v1/experiments/{self._id}/trials")["trials"]
+        return [Trial(self._session, r["id"], r) for r in rows]
+
+    get_trials = list_trials
+
+    def iter_trials(self) -> Iterator[Trial]:
+        yield from self.list_trials()
+
+    def await_first_trial(self, interval: float = 0.1, timeout: float = 600.0) -> Trial:
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            ts = self.list_trials()
+            if ts:
+                return ts[0]
+            time.sleep(interval)
+        raise TimeoutError(f"experiment {self._id} created no trial within {timeout}s")
+
+    def wait(self, interval: float = 5.0, timeout: Optional[float] = None) -> ExperimentState:
+        t0 = time.time()
+        while True:
+            self.reload()
+            if self.state in TERMINAL:
+                return self.state
+            if timeout is not None and time.time() - t0 > timeout:
+                raise TimeoutError(f"experiment {self._id} still {self.state.value}")
+            time.sleep(interval)
+
+    def list_checkpoints(self, sort_by: Optional[str] = None, smaller_is_better: Optional[bool] = None,
+                         max_results: Optional[int] = None) -> List[Checkpoint]:
+        rows = self._session.get(f"/api/v1/experiments/{self._id}/checkpoints")["checkpoints"]
+        cks = [Checkpoint(self._session, r["uuid"], r) for r in rows if r.get("state", "COMPLETED") != "DELETED"]
+        if sort_by is not None or smaller_is_better is not None:
+            cks = _best(cks, self._session, self._id, sort_by, smaller_is_better)
+        return cks[:max_results] if max_results else cks
+
+    def top_checkpoint(self, sort_by: Optional[str] = None, smaller_is_better: Optional[bool] = None) -> Checkpoint:
+        cks = self.top_n_checkpoints(1, sort_by, smaller_is_better)
+        if not cks:
+            raise RuntimeError(f"experiment {self._id} has no checkpoints")
+        return cks[0]
+
+    def top_n_checkpoints(self, limit: int, sort_by: Optional[str] = None,
+                          smaller_is_better: Optional[bool] = None) -> List[Checkpoint]:
+        cks = self.list_checkpoints()
+        return _best(cks, self._session, self._id, sort_by, smaller_is_better)[:limit]
+
+    def __repr__(self) -> str:
+        return f"Experiment(id={self._id})"
+
+
+def create_experiment(config: Union[str, pathlib.Path, Dict[str, Any]], model_dir: Optional[str] = None,
+                      includes: Optional[Iterable[Union[str, pathlib.Path]]] = None, parent_id: Optional[int] = None,
+                      activate: bool = True) -> Experiment:
+    if isinstance(config, (str, pathlib.Path)):
+        with open(config) as f:
+            config = yaml.safe_load(f)
+    body: Dict[str, Any] = {"config": config, "activate": activate, "parent_id": parent_id}
+    if model_dir is not None:
+        body["model_def"] = base64.b64encode(_tar_dir(model_dir)).decode()
+    r = _s().post("/api/v1/experiments", body)
+    return Experiment(_s(), r["experiment"]["id"], r["experiment"])
+
+
+def get_experiment(experiment_id: int) -> Experiment:
+    return Experiment(_s(), experiment_id)
+
+
+def list_experiments(archived: Optional[bool] = None, name: Optional[str] = None) -> List[Experiment]:
+    params = {} if archived is None else {"archived": str(archived).lower()}
+    rows = _s().get("/api/v1/experiments", params=params)["experiments"]
+    return [Experiment(_s(), r["id"], r) for r in rows if name is None or r.get("name") == name]
+
+
+def get_trial(trial_id: int) -> Trial:
+    return Trial(_s(), trial_id)
+
+
+def get_checkpoint(uuid: str) -> Checkpoint:
+    return Checkpoint(_s(), uuid)
+
+
+# ---------------------------------------------------------------------------------------------
+# model registry
+# ---------------------------------------------------------------------------------------------
+class ModelVersion:
+    def __init__(self, session: Session, model_name: str, data: Dict[str, Any]) -> None:
+        self._session = session
+        self.model_name = model_name
+        self._data = data
+
+    @property
+    def model_version(self) -> int:
+        return int(self._data["version"])
+
+    @property
+    def name(self) -> str:
+        return self._data.get("name") or ""
+
+    @property
+    def notes(self) -> str:
+        return self._data.get("comment") or ""
+
+    @property
+    def checkpoint(self) -> Checkpoint:
+        return Checkpoint(self._session, self._data["checkpoint_uuid"])
+
+    def _path(self) -> str:
+        return f"/api/v1/models/{self.model_name}/versions/{self.model_version}"
+
+    def set_name(self, name: str) -> None:
+        self._session.patch(self._path(), {"name": name})
+        self._data["name"] = name
+
+    def set_notes(self, notes: str) -> None:
+        self._session.patch(self._path(), {"notes": notes})
+        self._data["comment"] = notes
+
+    def delete(self) -> None:
+        self._session.delete(self._path())
+
+    def get_metrics(self, group: Optional[str] = None) -> Iterable[Dict[str, Any]]:
+        return self.checkpoint.get_metrics(group)
+
+    def __repr__(self) -> str:
+        return f"ModelVersion({self.model_name}, v{self.model_version})"
+
+
+class Model:
+    def __init__(self, session: Session, data: Dict[str, Any]) -> None:
+        self._session = session
+        self._data = data
+
+    @property
+    def name(self) -> str:
+        return self._data["name"]
+
+    @property
+    def model_id(self) -> int:
+        return int(self._data["id"])
+
+    @property
+    def description(self) -> str:
+        return self._data.get("description") or ""
+
+    @property
+    def metadata(self) -> Dict[str, Any]:
+        return dict(self._data.get("metadata") or {})
+
+    @property
+    def labels(self) -> List[str]:
+        return list(self._data.get("labels") or [])
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/models/{self.name}")["model"]
+
+    def list_versions(self) -> List[ModelVersion]:
+        rows = self._session.get(f"/api/v1/models/{self.name}/versions")["model_versions"]
+        return [ModelVersion(self._session, self.name, r) for r in sorted(rows, key=lambda r: -r["version"])]
+
+    get_versions = list_versions
+
+    def get_version(self, version: int = -1) -> Optional[ModelVersion]:
+        vs = self.list_versions()
+        if not vs:
+            return None
+        if version == -1:
+            return vs[0]
+        return next((v for v in vs if v.model_version == version), None)
+
+    def register_version(self, checkpoint_uuid: str) -> ModelVersion:
+        r = self._session.post(f"/api/v1/models/{self.name}/versions", {"checkpoint_uuid": checkpoint_uuid})
+        return ModelVersion(self._session, self.name, r["model_version"])
+
+    def _patch(self, **cols: Any) -> None:
+        self._session.patch(f"/api/v1/models/{self.name}", cols)
+        self._data.update(cols)
+
+    def set_description(self, description: str) -> None:
+        self._patch(description=description)
+
+    def add_metadata(self, metadata: Dict[str, Any]) -> None:
+        md = self.metadata
+        md.update(metadata)
+        self._patch(metadata=md)
+
+    def remove_metadata(self, keys: List[str]) -> None:
+        self._patch(metadata={k: v for k, v in self.metadata.items() if k not in keys})
+
+    def set_labels(self, labels: List[str]) -> None:
+        self._patch(labels=list(labels))
+
+    def archive(self) -> None:
+        self._patch(archived=1)
+
+    def unarchive(self) -> None:
+        self._patch(archived=0)
+
+    def delete(self) -> None:
+        self._session.delete(f"/api/v1/models/{self.name}")
+
+    def __repr__(self) -> str:
+        return f"Model(name={self.name})"
+
+
+def create_model(name: str, description: str = "", metadata: Optional[Dict[str, Any]] = None,
+                 labels: Optional[List[str]] = None) -> Model:
+    r = _s().post("/api/v1/models", {"name": name, "description": description, "metadata": metadata or {},
+                                     "labels": labels or []})
+    return Model(_s(), r["model"])
+
+
+def get_model(identifier: Union[str, int]) -> Model:
+    if isinstance(identifier, int):
+        for m in list_models():
+            if m.model_id == identifier:
+                return m
+        raise NotFoundException(404, f"model {identifier} not found")
+    return Model(_s(), _s().get(f"/api/v1/models/{identifier}")["model"])
+
+
+def list_models(name: Optional[str] = None, labels: Optional[List[str]] = None) -> List[Model]:
+    rows = _s().get("/api/v1/models")["models"]
+    out = [Model(_s(), r) for r in rows]
+    if name is not None:
+        out = [m for m in out if m.name == name]
+    if labels:
+        out = [m for m in out if set(labels) <= set(m.labels)]
+    return out
+
+
+get_models = list_models
+
+
+def get_model_labels() -> List[str]:
+    return sorted({lab for m in list_models() for lab in m.labels})
+
+
+def stream_trials_training_metrics(trial_ids: List[int]) -> Iterable[Dict[str, Any]]:
+    for tid in trial_ids:
+        yield from Trial(_s(), tid).iter_metrics("training")
+
+
+def stream_trials_validation_metrics(trial_ids: List[int]) -> Iterable[Dict[str, Any]]:
+    for tid in trial_ids:
+        yield from Trial(_s(), tid).iter_metrics("validation")
+
+
+def iter_trials_metrics(trial_ids: List[int], group: str) -> Iterable[Dict[str, Any]]:
+    for tid in trial_ids:
+        yield from Trial(_s(), tid).iter_metrics(group)

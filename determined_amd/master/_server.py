@@ -262,6 +262,14 @@ def build_routes(m: Master) -> List[Route]:
         row["checkpoint_storage"] = (exp or {}).get("config", {}).get("checkpoint_storage") if exp else None
         return {"checkpoint": row}
 
+    @route("PATCH", r"/api/v1/checkpoints/([0-9a-f\-]+)")
+    def patch_ckpt(q, b, u):
+        if m.db.one("SELECT uuid FROM checkpoints WHERE uuid=?", [u]) is None:
+            raise HTTPError(404, f"checkpoint {u} not found")
+        if "metadata" in b:
+            m.db.update("checkpoints", "uuid", u, metadata=b["metadata"])
+        return {}
+
     @route("DELETE", r"/api/v1/checkpoints/([0-9a-f\-]+)")
     def del_ckpt(q, b, u):
         m.delete_checkpoints([u])
@@ -418,6 +426,29 @@ def build_routes(m: Master) -> List[Route]:
             raise HTTPError(404, "model not found")
         return {"model_versions": m.db.all("SELECT * FROM model_versions WHERE model_id=? ORDER BY version",
                                            [row["id"]])}
+
+    def _version_row(name: str, ver: str) -> Dict[str, Any]:
+        mrow = m.db.one("SELECT id FROM models WHERE name=?", [urllib.parse.unquote(name)])
+        row = m.db.one("SELECT * FROM model_versions WHERE model_id=? AND version=?", [mrow["id"], int(ver)]) \
+            if mrow else None
+        if row is None:
+            raise HTTPError(404, f"model version {name}/{ver} not found")
+        return row
+
+    @route("PATCH", r"/api/v1/models/([^/]+)/versions/(\d+)")
+    def patch_version(q, b, name, ver):
+        row = _version_row(name, ver)
+        cols = {k: v for k, v in b.items() if k in ("name", "comment", "metadata", "notes")}
+        if "notes" in cols:
+            cols["comment"] = cols.pop("notes")
+        m.db.update("model_versions", "id", row["id"], **cols)
+        return {}
+
+    @route("DELETE", r"/api/v1/models/([^/]+)/versions/(\d+)")
+    def del_version(q, b, name, ver):
+        row = _version_row(name, ver)
+        m.db.execute("DELETE FROM model_versions WHERE id=?", [row["id"]])
+        return {}
 
     # ---------------------------------------------------------------- webhooks / templates
     @route("POST", "/api/v1/webhooks")

@@ -155,3 +155,39 @@ def test_grid_and_model_registry_and_cli(cluster):
     with contextlib.redirect_stdout(out):
         det(["-m", cluster["url"], "agent", "list"])
     assert "e2e-agent" in out.getvalue()
+
+
+def test_sdk_client(cluster):
+    from determined_amd.experimental import client
+
+    client.login(cluster["url"])
+    exp = client.create_experiment(
+        {"name": "sdk", "hyperparameters": HP, "entrypoint": "model_def:TinyTrial",
+         "checkpoint_storage": {"type": "shared_fs", "host_path": cluster["ckpt"]},
+         "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": 8}},
+         "min_validation_period": {"batches": 4}}, str(TINY))
+    assert exp.wait(interval=0.5, timeout=180) == client.ExperimentState.COMPLETED
+    exp.add_label("fast")
+    exp.set_description("sdk test")
+    exp.reload()
+    assert "fast" in exp.labels
+    (trial,) = exp.list_trials()
+    assert trial.state == client.TrialState.COMPLETED
+    assert list(trial.stream_validation_metrics())
+    assert any(trial.logs())
+    best = exp.top_checkpoint()
+    assert best.steps_completed in (4, 8)
+    with tempfile.TemporaryDirectory() as d:
+        p = best.download(os.path.join(d, "ck"))
+        assert os.path.exists(os.path.join(p, "state_dict.pth"))
+        code = exp.download_code(os.path.join(d, "code"))
+        assert os.path.exists(os.path.join(code, "model_def.py"))
+    best.add_metadata({"note": "best"})
+    assert client.get_checkpoint(best.uuid).metadata["note"] == "best"
+    model = client.create_model("sdk-model", labels=["x"])
+    v = model.register_version(best.uuid)
+    v.set_notes("first")
+    assert model.get_version().model_version == 1 and model.get_version().notes == "first"
+    assert [m.name for m in client.list_models(labels=["x"])] == ["sdk-model"]
+    v.delete()
+    assert model.get_version() is None
