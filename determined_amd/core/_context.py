@@ -117,9 +117,12 @@ def _dummy_init(*, distributed: Optional[DistributedContext] = None,
 def init(*, distributed: Optional[DistributedContext] = None,
          checkpoint_storage: Optional[Union[str, Dict[str, Any]]] = None,
          preempt_mode: PreemptMode = PreemptMode.WorkersAskChief,
-         tensorboard_mode: Any = None) -> Context:
-    """Build a core.Context; on-cluster it talks to the master, off-cluster it runs locally."""
-    info = get_cluster_info()
+         tensorboard_mode: Any = None, _info: Any = None, _unmanaged: bool = False) -> Context:
+    """Build a core.Context; on-cluster it talks to the master, off-cluster it runs locally.
+
+    ``_info``/``_unmanaged`` are used by ``experimental.core_v2`` for unmanaged trials: the
+    process runs outside the cluster but reports metrics and checkpoints to the master."""
+    info = _info if _info is not None else get_cluster_info()
     if info is None:
         return _dummy_init(distributed=distributed, checkpoint_storage=checkpoint_storage,
                            preempt_mode=preempt_mode)
@@ -146,6 +149,13 @@ def init(*, distributed: Optional[DistributedContext] = None,
             logger.debug(f"tensorboard disabled: {e}")
         train = TrainContext(session, info.trial.trial_id, info.trial._trial_run_id, info.trial.experiment_id,
                              distributed, tb, tbd_writer)
+        if _unmanaged:
+            checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,
+                                           info.trial.trial_id, tb)
+            _install_stacktrace_on_sigusr1()
+            return Context(checkpoint=checkpoint, distributed=distributed,
+                           preempt=DummyPreemptContext(distributed, preempt_mode), train=train,
+                           searcher=DummySearcherContext(distributed, 10**9), info=info, _tensorboard_manager=tb)
         searcher = SearcherContext(session, distributed, info.trial.trial_id, info.trial._trial_run_id,
                                    info.allocation_id, _parse_searcher_units(cfg))
         checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,

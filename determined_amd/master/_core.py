@@ -131,7 +131,9 @@ class Master:
             cfg = row["config"]
             exp = ExperimentRec(row["id"], cfg, row["state"])
             self.experiments[exp.id] = exp
-            if cfg["searcher"]["name"] != "custom":
+            if row.get("unmanaged"):
+                exp.unmanaged = True  # type: ignore[attr-defined]
+            elif cfg["searcher"]["name"] != "custom":
                 from determined_amd.searcher import Searcher
 
                 exp.searcher = Searcher(cfg["searcher"], cfg.get("hyperparameters", {}),
@@ -179,6 +181,72 @@ class Master:
             self._fire_webhooks(exp, "EXPERIMENT_STATE_CHANGE")
             self.cv.notify_all()
             return eid
+
+    # ---------------------------------------------------------------- unmanaged (core_v2)
+    def create_unmanaged_experiment(self, cfg: Dict[str, Any], external_id: Optional[str] = None) -> int:
+        """Experiment whose trials run outside the cluster and only report (no searcher, no
+        allocations); ``external_id`` makes the call idempotent (resume / multi-trial grouping)."""
+        with self.lock:
+            if external_id:
+                row = self.db.one("SELECT id FROM experiments WHERE external_id=?", [external_id])
+                if row is not None:
+                    return int(row["id"])
+            cfg = dict(cfg)
+            cfg.setdefault("entrypoint", "unmanaged")
+            cfg = expconf.parse(cfg)
+            eid = self.db.insert("experiments", name=cfg["name"], state="ACTIVE", config=cfg, model_def=None,
+                                 start_time=time.time(), description=cfg.get("description") or "",
+                                 labels=cfg.get("labels") or [], unmanaged=1, external_id=external_id,
+                                 project=cfg.get("project") or "Uncategorized",
+                                 workspace=cfg.get("workspace") or "Uncategorized")
+            exp = ExperimentRec(eid, cfg, "ACTIVE")
+            exp.unmanaged = True  # type: ignore[attr-defined]
+            self.experiments[eid] = exp
+            return eid
+
+    def create_unmanaged_trial(self, eid: int, hparams: Dict[str, Any],
+                               external_id: Optional[str] = None) -> Dict[str, Any]:
+        with self.lock:
+            exp = self.experiments.get(eid)
+            if exp is None:  # finished earlier (or before a master restart): re-register to resume
+                exp = self._exp(eid)
+                exp.unmanaged = True  # type: ignore[attr-defined]
+                for t in self.db.all("SELECT * FROM trials WHERE experiment_id=?", [eid]):
+                    tr = TrialRec(t["id"], eid, t["request_id"], t["hparams"], t["seed"])
+                    tr.state, tr.total_batches = t["state"], t["total_batches"] or 0
+                    tr.latest_checkpoint = t["latest_checkpoint"]
+                    exp.trials[tr.request_id] = tr
+                self.experiments[eid] = exp
+            if external_id:
+                row = self.db.one("SELECT * FROM trials WHERE experiment_id=? AND external_id=?", [eid, external_id])
+                if row is not None:
+                    tr = next((t for t in exp.trials.values() if t.id == row["id"]), None)
+                    if tr is not None and tr.state in TERMINAL_TRIAL:
+                        tr.state = "ACTIVE"  # resumed
+                        self._persist_trial(tr)
+                    if exp.state in TERMINAL_EXP:
+                        exp.state = "ACTIVE"
+                        self.db.update("experiments", "id", eid, state="ACTIVE", end_time=None)
+                    return {"trial_id": row["id"], "latest_checkpoint": row.get("latest_checkpoint"),
+                            "steps_completed": row.get("total_batches") or 0}
+            rid = len(exp.trials) + 1
+            while rid in exp.trials:
+                rid += 1
+            seed = (exp.config["reproducibility"]["experiment_seed"] + rid) % (2**31)
+            tid = self.db.insert("trials", experiment_id=eid, request_id=rid, state="ACTIVE", hparams=hparams or {},
+                                 seed=seed, start_time=time.time(), external_id=external_id)
+            tr = TrialRec(tid, eid, rid, hparams or {}, seed)
+            exp.trials[rid] = tr
+            return {"trial_id": tid, "latest_checkpoint": None, "steps_completed": 0}
+
+    def close_unmanaged_trial(self, tid: int, state: str = "COMPLETED") -> None:
+        with self.lock:
+            exp, tr = self._trial(tid)
+            tr.state = state if state in TERMINAL_TRIAL else "COMPLETED"
+            self._persist_trial(tr)
+            if all(t.state in TERMINAL_TRIAL for t in exp.trials.values()):
+                self._set_exp_state(exp, "ERROR" if all(t.state == "ERROR" for t in exp.trials.values())
+                                    else "COMPLETED")
 
     def _persist_exp(self, exp: ExperimentRec) -> None:
         snap = exp.searcher.snapshot() if exp.searcher is not None else None

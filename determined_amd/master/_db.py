@@ -46,6 +46,8 @@ CREATE TABLE IF NOT EXISTS webhooks (
 CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
 """
 
+MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT")]
+
 JSON_COLS = {"config", "hparams", "metrics", "batch_metrics", "resources", "metadata", "searcher_snapshot", "labels",
              "searcher_state", "triggers"}
 
@@ -58,6 +60,11 @@ class DB:
         if path != ":memory:":
             self.conn.execute("PRAGMA journal_mode=WAL")
         self.conn.executescript(SCHEMA)
+        for table, col, decl in MIGRATIONS:  # columns added after a database file was created
+            try:
+                self.conn.execute(f"ALTER TABLE {table} ADD COLUMN {col} {decl}")
+            except sqlite3.OperationalError:
+                pass
         self.lock = threading.RLock()
 
     def _row(self, r: Optional[sqlite3.Row]) -> Optional[Dict[str, Any]]:

@@ -95,6 +95,23 @@ def build_routes(m: Master) -> List[Route]:
             raise HTTPError(400, str(e))
         return {"experiment": _exp_summary(m, m.db.one("SELECT * FROM experiments WHERE id=?", [eid]))}
 
+    @route("POST", "/api/v1/unmanaged/experiments")
+    def create_unmanaged_exp(q, b):
+        try:
+            eid = m.create_unmanaged_experiment(b["config"], b.get("external_experiment_id"))
+        except InvalidConfig as e:
+            raise HTTPError(400, str(e))
+        return {"experiment": _exp_summary(m, m.db.one("SELECT * FROM experiments WHERE id=?", [eid]))}
+
+    @route("POST", r"/api/v1/unmanaged/experiments/(\d+)/trials")
+    def create_unmanaged_trial(q, b, eid):
+        return m.create_unmanaged_trial(int(eid), b.get("hparams") or {}, b.get("external_trial_id"))
+
+    @route("POST", r"/api/v1/unmanaged/trials/(\d+)/close")
+    def close_unmanaged_trial(q, b, tid):
+        m.close_unmanaged_trial(int(tid), b.get("state", "COMPLETED"))
+        return {}
+
     @route("GET", "/api/v1/experiments")
     def list_exps(q, b):
         rows = m.db.all("SELECT * FROM experiments WHERE state!='DELETED' ORDER BY id")

@@ -191,3 +191,31 @@ def test_sdk_client(cluster):
     assert [m.name for m in client.list_models(labels=["x"])] == ["sdk-model"]
     v.delete()
     assert model.get_version() is None
+
+
+def test_core_v2_unmanaged(cluster):
+    from determined_amd.experimental import client, core_v2
+
+    defaults = core_v2.DefaultConfig(name="unmanaged-run", hparams={"lr": 0.5},
+                                     checkpoint_storage={"type": "shared_fs", "host_path": cluster["ckpt"]})
+    um = core_v2.UnmanagedConfig(external_experiment_id="ext-exp-1", external_trial_id="ext-trial-1")
+    core_v2.init(defaults=defaults, unmanaged=um, master=cluster["url"])
+    tid = core_v2.info.trial.trial_id
+    eid = core_v2.info.trial.experiment_id
+    for step in (1, 2, 3):
+        core_v2.train.report_training_metrics(steps_completed=step, metrics={"loss": 1.0 / step})
+    core_v2.train.report_validation_metrics(steps_completed=3, metrics={"unmanaged": 0.25})
+    with core_v2.checkpoint.store_path({"steps_completed": 3}) as (path, uuid):
+        (path / "w.txt").write_text("weights")
+    core_v2.close()
+    client.login(cluster["url"])
+    exp = client.get_experiment(eid)
+    assert exp.state == client.ExperimentState.COMPLETED
+    (t,) = exp.list_trials()
+    assert t.id == tid and t.hparams == {"lr": 0.5}
+    assert len(list(t.stream_training_metrics())) == 3
+    assert [c.uuid for c in t.list_checkpoints()] == [uuid]
+    # resuming with the same external ids reuses the experiment and trial
+    core_v2.init(defaults=defaults, unmanaged=um, master=cluster["url"])
+    assert core_v2.info.trial.trial_id == tid and core_v2.info.latest_checkpoint == uuid
+    core_v2.close()
