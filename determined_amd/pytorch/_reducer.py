@@ -85,12 +85,16 @@ class _PyTorchReducerContext:
                      for_training: bool = True, for_validation: bool = True) -> MetricReducer:
         if not isinstance(reducer, MetricReducer):
             reducer = _SimpleReducer(reducer)
-        self._wrapped_reducers.append(_WrappedReducer(reducer, name))
+        w = _WrappedReducer(reducer, name)
+        w.for_training, w.for_validation = for_training, for_validation  # type: ignore[attr-defined]
+        self._wrapped_reducers.append(w)
         return reducer
 
     def reduce_metrics(self, for_training: bool) -> Dict[str, Any]:
         out: Dict[str, Any] = {}
         for w in self._wrapped_reducers:
+            if not getattr(w, "for_training" if for_training else "for_validation", True):
+                continue
             per_slot = self._allgather_fn(w.reducer.per_slot_reduce())
             val = w.reducer.cross_slot_reduce(per_slot)
             if w.name is None:
