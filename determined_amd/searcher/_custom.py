@@ -14,7 +14,6 @@ import io
 import json
 import logging
 import pathlib
-import pickle
 import tarfile
 import time
 import uuid

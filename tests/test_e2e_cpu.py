@@ -219,3 +219,56 @@ def test_core_v2_unmanaged(cluster):
     core_v2.init(defaults=defaults, unmanaged=um, master=cluster["url"])
     assert core_v2.info.trial.trial_id == tid and core_v2.info.latest_checkpoint == uuid
     core_v2.close()
+
+
+def test_custom_searcher_local_runner(cluster):
+    import uuid as uuidlib
+
+    from determined_amd import searcher as det_searcher
+
+    class TwoTrials(det_searcher.SearchMethod):
+        def __init__(self):
+            self.created = 0
+
+        def initial_operations(self, st):
+            ops = []
+            for lr in (0.05, 0.2):
+                rid = uuidlib.uuid4()
+                ops += [det_searcher.Create(rid, {"lr": lr, "global_batch_size": 16}, checkpoint=None),
+                        det_searcher.ValidateAfter(rid, 4)]
+            return ops
+
+        def on_trial_created(self, st, rid):
+            self.created += 1
+            return []
+
+        def on_validation_completed(self, st, rid, metric, length):
+            if length < 8:
+                return [det_searcher.ValidateAfter(rid, 8)]
+            return [det_searcher.Close(rid)]
+
+        def on_trial_closed(self, st, rid):
+            if len(st.trials_closed) == 2:
+                return [det_searcher.Shutdown()]
+            return []
+
+        def progress(self, st):
+            return len(st.trials_closed) / 2
+
+        def on_trial_exited_early(self, st, rid, reason):
+            return [det_searcher.Shutdown(failure=True)]
+
+    from determined_amd.common.api import Session
+
+    with tempfile.TemporaryDirectory() as d:
+        method = TwoTrials()
+        runner = det_searcher.LocalSearchRunner(method, pathlib.Path(d), session=Session(cluster["url"]))
+        cfg = {"name": "custom", "entrypoint": "model_def:TinyTrial",
+               "checkpoint_storage": {"type": "shared_fs", "host_path": cluster["ckpt"]},
+               "searcher": {"name": "custom", "metric": "validation_loss"}, "hyperparameters": HP}
+        eid = runner.run(cfg, model_dir=str(TINY))
+        assert (pathlib.Path(d) / "searcher_state.json").exists()
+    e = _wait(cluster, eid)
+    assert e["state"] == "COMPLETED" and method.created == 2
+    ts = _trials(cluster, eid)
+    assert sorted(t["total_batches"] for t in ts) == [8, 8]
