@@ -1,0 +1,477 @@
+// Flash attention (forward + backward) for gfx950 / MI355X: bf16 in/out, fp32 accumulate,
+// online softmax, optional causal mask, head dim D in {64, 128}.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 (64-wide wave computes a 16x16 tile, K = 32).
+//   A operand: lane l holds A[row l&15][k 8(l>>4)+j], B operand: B[k 8(l>>4)+j][col l&15],
+//   C/D: C[row 4(l>>4)+r][col l&15], r = 0..3.
+//
+// Forward (one workgroup = 4 waves = 64 query rows, a wave = 16 rows):
+//   S^T = K.Q^T so the query sits on the lane (col) and 4 keys per 16-key tile sit in the
+//   lane's registers: the row max / row sum of the online softmax are in-lane + 2 xor
+//   shuffles, the running (m, l) and the rescale of O are lane-local, and O^T = V^T.P^T takes
+//   P^T straight from the S^T accumulators (no LDS round trip): a 32-key MFMA step permutes
+//   its k index as key(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4), and the V^T operand is read
+//   in that same order from a transposed LDS image Vt[d][key].
+//   K/V tiles (64 keys) are staged once per workgroup in LDS and shared by the 4 waves.
+//
+// Backward (one workgroup = 64 keys, a wave = 16 keys; loop over 64-row query blocks):
+//   S = Q.K^T and dP = dO.V^T with the key on the lane (K, V fragments of the wave's own keys
+//   stay in registers), P = exp2(S.scale.log2e - LSE.log2e), dS = P.(dP - delta); the
+//   accumulators feed dV^T = dO^T.P and dK^T = Q^T.dS directly (same k permutation, Q^T/dO^T
+//   from transposed LDS images); dS goes through LDS once for dQ = dS.K, which is added into
+//   an fp32 buffer with float atomics and converted to bf16 by a final pass.
+//
+// Strides are in elements for (batch, head, token); the head dimension must be contiguous.
+
+#include "common.h"
+
+#include <math.h>
+
+namespace damd {
+namespace attn {
+
+typedef short s8 __attribute__((ext_vector_type(8)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlk = 64;       // query rows per fwd workgroup == keys per bwd workgroup == kv tile
+constexpr int kThreads = 256;  // 4 waves
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+struct Strides {
+  int64_t b, h, t;
+};
+
+struct FwdArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
+  Strides sq, sk, sv, so;
+  int H, T;
+  float scale_log2;  // softmax scale * log2(e)
+};
+
+struct BwdArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dout;
+  const float* lse; const float* delta; float* dq_acc; bf16_t* dk; bf16_t* dv;
+  Strides sq, sk, sv, sdo, sdk, sdv;
+  int H, T;
+  float scale, scale_log2;
+};
+
+__device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ short bfs(float x) { return static_cast<short>(f2bf(x)); }
+
+// P^T / dS fragment of a 32-key (or 32-query) k step from two 16-wide accumulator tiles.
+__device__ __forceinline__ s8 pack_pair(f4 lo, f4 hi) {
+  s8 r;
+  r[0] = bfs(lo[0]); r[1] = bfs(lo[1]); r[2] = bfs(lo[2]); r[3] = bfs(lo[3]);
+  r[4] = bfs(hi[0]); r[5] = bfs(hi[1]); r[6] = bfs(hi[2]); r[7] = bfs(hi[3]);
+  return r;
+}
+
+// Operand read in the permuted k order from a transposed image row: keys 4g..4g+3 and
+// 16+4g..16+4g+3 of the 32-wide step starting at `row`.
+__device__ __forceinline__ s8 read_perm(const bf16_t* row, int g) {
+  const s4 lo = *reinterpret_cast<const s4*>(row + 4 * g);
+  const s4 hi = *reinterpret_cast<const s4*>(row + 16 + 4 * g);
+  s8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// Cooperative 64 x D tile load: row-major image (row stride D+8) and/or transposed image
+// (row stride 64+8).  Rows >= T are zero.
+template <int D, bool ROW, bool TRANS>
+__device__ __forceinline__ void load_tile(const bf16_t* __restrict__ base, int64_t st, int r0, int T,
+                                          bf16_t* rowimg, bf16_t* trimg) {
+  constexpr int CH = D / 8;
+  for (int i = threadIdx.x; i < kBlk * CH; i += kThreads) {
+    const int r = i / CH, c = (i % CH) * 8;
+    s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + r < T) x = *reinterpret_cast<const s8*>(base + static_cast<int64_t>(r0 + r) * st + c);
+    if (ROW) *reinterpret_cast<s8*>(rowimg + r * (D + 8) + c) = x;
+    if (TRANS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) trimg[(c + j) * (kBlk + 8) + r] = x[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
+  constexpr int KP = D + 8, VP = kBlk + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[D * VP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int T = a.T, nblk = (T + kBlk - 1) / kBlk;
+  const int qb = CAUSAL ? (nblk - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = qb * kBlk;
+  const bf16_t* Qp = a.q + b * a.sq.b + h * a.sq.h;
+  const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
+  const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
+  const int myq = q0 + w * 16 + c;  // query whose softmax state this lane carries
+
+  s8 qf[D / 32];
+#pragma unroll
+  for (int ds = 0; ds < D / 32; ++ds) {
+    s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (myq < T) x = *reinterpret_cast<const s8*>(Qp + static_cast<int64_t>(myq) * a.sq.t + ds * 32 + 8 * g);
+    qf[ds] = x;
+  }
+  f4 oacc[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) oacc[dt] = f4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int kb_end = CAUSAL ? min(nblk, (q0 + kBlk - 1) / kBlk + 1) : nblk;
+  for (int kb = 0; kb < kb_end; ++kb) {
+    const int k0 = kb * kBlk;
+    __syncthreads();
+    load_tile<D, true, false>(Kp, a.sk.t, k0, T, Ks, nullptr);
+    load_tile<D, false, true>(Vp, a.sv.t, k0, T, nullptr, Vt);
+    __syncthreads();
+
+    f4 s[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      s[nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < D / 32; ++ds) {
+        const s8 kf = *reinterpret_cast<const s8*>(Ks + (nt * 16 + c) * KP + ds * 32 + 8 * g);
+        s[nt] = mfma(kf, qf[ds], s[nt]);
+      }
+    }
+    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && k0 + kBlk - 1 > q0 + w * 16);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = s[nt][r] * a.scale_log2;
+        if (need_mask) {
+          const int key = k0 + nt * 16 + 4 * g + r;
+          if (key >= T || (CAUSAL && key > myq)) v = -INFINITY;
+        }
+        s[nt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m - m_use);
+    float rs = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[nt][r] - m_use);
+        s[nt][r] = p;
+        rs += p;
+      }
+    }
+    l = l * alpha + rs;
+    m = m_new;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const s8 pb = pack_pair(s[2 * s2], s[2 * s2 + 1]);
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const s8 vf = read_perm(Vt + (dt * 16 + c) * VP + s2 * 32, g);
+        oacc[dt] = mfma(vf, pb, oacc[dt]);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (myq < T) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* Op = a.o + b * a.so.b + h * a.so.h + static_cast<int64_t>(myq) * a.so.t;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      s4 ov;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ov[r] = bfs(oacc[dt][r] * inv);
+      *reinterpret_cast<s4*>(Op + dt * 16 + 4 * g) = ov;
+    }
+    if (g == 0)
+      a.lse[(static_cast<int64_t>(b) * a.H + h) * T + myq] = l > 0.f ? m * kLn2 + logf(l) : -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+// delta[b,h,t] = sum_d dO * O  (D/8 lanes per row, one 16-byte chunk each)
+template <int D>
+__global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ o, Strides so,
+                                                         const bf16_t* __restrict__ dout, Strides sd,
+                                                         float* __restrict__ delta, int H, int T, int64_t rows) {
+  constexpr int L = D / 8;
+  const int64_t row = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) / L;
+  const int part = threadIdx.x % L;
+  float acc = 0.f;
+  if (row < rows) {
+    const int t = static_cast<int>(row % T);
+    const int64_t bh = row / T;
+    const int h = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
+    const s8 x = *reinterpret_cast<const s8*>(o + b * so.b + h * so.h + t * so.t + part * 8);
+    const s8 y = *reinterpret_cast<const s8*>(dout + b * sd.b + h * sd.h + t * sd.t + part * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f(static_cast<bf16_t>(x[j])) * bf2f(static_cast<bf16_t>(y[j]));
+  }
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (row < rows && part == 0) delta[row] = acc;
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
+  constexpr int RP = D + 8, TP = kBlk + 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem_raw);  // [64][RP]
+  bf16_t* dOs = Qs + kBlk * RP;                       // [64][RP]
+  bf16_t* Qt = dOs + kBlk * RP;                       // [D][TP]
+  bf16_t* dOt = Qt + D * TP;                          // [D][TP]
+  bf16_t* Kt = dOt + D * TP;                          // [D][TP]  (this workgroup's keys)
+  bf16_t* dSs = Kt + D * TP;                          // [64 q][TP]
+  float* lse2 = reinterpret_cast<float*>(dSs + kBlk * TP);  // [64]
+  float* dl = lse2 + kBlk;                                  // [64]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int T = a.T, nblk = (T + kBlk - 1) / kBlk;
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int k0 = kb * kBlk;
+  const bf16_t* Qp = a.q + b * a.sq.b + h * a.sq.h;
+  const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
+  const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
+  const bf16_t* dOp = a.dout + b * a.sdo.b + h * a.sdo.h;
+  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+  const int mykey = k0 + w * 16 + c;
+
+  s8 kf[D / 32], vf[D / 32];
+#pragma unroll
+  for (int ds = 0; ds < D / 32; ++ds) {
+    s8 x = {0, 0, 0, 0, 0, 0, 0, 0}, y = x;
+    if (mykey < T) {
+      x = *reinterpret_cast<const s8*>(Kp + static_cast<int64_t>(mykey) * a.sk.t + ds * 32 + 8 * g);
+      y = *reinterpret_cast<const s8*>(Vp + static_cast<int64_t>(mykey) * a.sv.t + ds * 32 + 8 * g);
+    }
+    kf[ds] = x;
+    vf[ds] = y;
+  }
+  load_tile<D, false, true>(Kp, a.sk.t, k0, T, nullptr, Kt);
+  f4 dk[D / 16], dv[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) dk[dt] = dv[dt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int qb = CAUSAL ? kb : 0; qb < nblk; ++qb) {
+    const int q0 = qb * kBlk;
+    __syncthreads();
+    load_tile<D, true, true>(Qp, a.sq.t, q0, T, Qs, Qt);
+    load_tile<D, true, true>(dOp, a.sdo.t, q0, T, dOs, dOt);
+    if (threadIdx.x < kBlk) {
+      const int q = q0 + threadIdx.x;
+      lse2[threadIdx.x] = q < T ? a.lse[bh * T + q] * kLog2e : INFINITY;
+      dl[threadIdx.x] = q < T ? a.delta[bh * T + q] : 0.f;
+    }
+    __syncthreads();
+
+    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && q0 < k0 + kBlk);
+    f4 P[4], dS[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      f4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < D / 32; ++ds) {
+        const s8 qa = *reinterpret_cast<const s8*>(Qs + (qt * 16 + c) * RP + ds * 32 + 8 * g);
+        const s8 oa = *reinterpret_cast<const s8*>(dOs + (qt * 16 + c) * RP + ds * 32 + 8 * g);
+        sacc = mfma(qa, kf[ds], sacc);
+        dpacc = mfma(oa, vf[ds], dpacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qt * 16 + 4 * g + r;
+        float p = exp2f(sacc[r] * a.scale_log2 - lse2[ql]);
+        if (need_mask && (mykey >= T || (CAUSAL && mykey > q0 + ql))) p = 0.f;
+        P[qt][r] = p;
+        dS[qt][r] = p * (dpacc[r] - dl[ql]);
+      }
+    }
+    // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = 32 queries per step, permuted order)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const s8 pb = pack_pair(P[2 * s2], P[2 * s2 + 1]);
+      const s8 sb = pack_pair(dS[2 * s2], dS[2 * s2 + 1]);
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        dv[dt] = mfma(read_perm(dOt + (dt * 16 + c) * TP + s2 * 32, g), pb, dv[dt]);
+        dk[dt] = mfma(read_perm(Qt + (dt * 16 + c) * TP + s2 * 32, g), sb, dk[dt]);
+      }
+    }
+    // dS -> LDS [q][key] for dQ = dS . K
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dSs[(qt * 16 + 4 * g + r) * TP + w * 16 + c] = static_cast<bf16_t>(bfs(dS[qt][r]));
+    }
+    __syncthreads();
+    f4 dq[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) dq[dt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const s8 sa = *reinterpret_cast<const s8*>(dSs + (w * 16 + c) * TP + ks * 32 + 8 * g);
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const s8 kt = *reinterpret_cast<const s8*>(Kt + (dt * 16 + c) * TP + ks * 32 + 8 * g);
+        dq[dt] = mfma(sa, kt, dq[dt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + w * 16 + 4 * g + r;
+      if (q < T) {
+        float* dst = a.dq_acc + (bh * T + q) * D + c;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt) atomicAdd(dst + dt * 16, dq[dt][r] * a.scale);
+      }
+    }
+  }
+  if (mykey < T) {
+    bf16_t* dKp = a.dk + b * a.sdk.b + h * a.sdk.h + static_cast<int64_t>(mykey) * a.sdk.t;
+    bf16_t* dVp = a.dv + b * a.sdv.b + h * a.sdv.h + static_cast<int64_t>(mykey) * a.sdv.t;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      s4 kv, vv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        kv[r] = bfs(dk[dt][r] * a.scale);
+        vv[r] = bfs(dv[dt][r]);
+      }
+      *reinterpret_cast<s4*>(dKp + dt * 16 + 4 * g) = kv;
+      *reinterpret_cast<s4*>(dVp + dt * 16 + 4 * g) = vv;
+    }
+  }
+}
+
+// dq[b,t,h,:] (strided bf16) = dq_acc[b,h,t,:] (fp32, contiguous)
+template <int D>
+__global__ void __launch_bounds__(256) attn_dq_convert_kernel(const float* __restrict__ acc, bf16_t* __restrict__ dq,
+                                                              Strides s, int H, int T, int64_t n8) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const int64_t e = i * 8;
+  const int d = static_cast<int>(e % D);
+  const int64_t row = e / D;
+  const int t = static_cast<int>(row % T);
+  const int64_t bh = row / T;
+  const int h = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
+  const float4 x0 = *reinterpret_cast<const float4*>(acc + e);
+  const float4 x1 = *reinterpret_cast<const float4*>(acc + e + 4);
+  s8 o;
+  o[0] = bfs(x0.x); o[1] = bfs(x0.y); o[2] = bfs(x0.z); o[3] = bfs(x0.w);
+  o[4] = bfs(x1.x); o[5] = bfs(x1.y); o[6] = bfs(x1.z); o[7] = bfs(x1.w);
+  *reinterpret_cast<s8*>(dq + b * s.b + h * s.h + t * s.t + d) = o;
+}
+
+template <int D>
+constexpr size_t bwd_smem_bytes() {
+  return sizeof(bf16_t) * (2 * kBlk * (D + 8) + 3 * D * (kBlk + 8) + kBlk * (kBlk + 8)) + 2 * kBlk * sizeof(float);
+}
+
+}  // namespace attn
+}  // namespace damd
+
+using namespace damd;
+using namespace damd::attn;
+
+extern "C" {
+
+// strides: 4 tensors (q, k, v, o) x (b, h, t) in elements
+void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
+                          int B, int H, int T, int D, float scale, int causal, hipStream_t st) {
+  FwdArgs a;
+  a.q = static_cast<const bf16_t*>(q); a.k = static_cast<const bf16_t*>(k); a.v = static_cast<const bf16_t*>(v);
+  a.o = static_cast<bf16_t*>(o); a.lse = lse;
+  a.sq = {strides[0], strides[1], strides[2]}; a.sk = {strides[3], strides[4], strides[5]};
+  a.sv = {strides[6], strides[7], strides[8]}; a.so = {strides[9], strides[10], strides[11]};
+  a.H = H; a.T = T; a.scale_log2 = scale * kLog2e;
+  dim3 grid((T + kBlk - 1) / kBlk, H, B);
+  if (D == 64) {
+    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
+  } else {
+    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
+  }
+  DAMD_CHECK_LAUNCH();
+}
+
+// strides: 7 tensors (q, k, v, o, dout, dk, dv) + dq  (8 x 3)
+void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                          const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
+                          const int64_t* s, int B, int H, int T, int D, float scale, int causal, hipStream_t st) {
+  const Strides sq{s[0], s[1], s[2]}, sk{s[3], s[4], s[5]}, sv{s[6], s[7], s[8]}, so{s[9], s[10], s[11]},
+      sdo{s[12], s[13], s[14]}, sdk{s[15], s[16], s[17]}, sdv{s[18], s[19], s[20]}, sdq{s[21], s[22], s[23]};
+  const int64_t rows = static_cast<int64_t>(B) * H * T;
+  (void)hipMemsetAsync(dq_acc, 0, sizeof(float) * rows * D, st);
+  {
+    const int64_t threads = rows * (D / 8);
+    const int blocks = static_cast<int>((threads + 255) / 256);
+    if (D == 64)
+      hipLaunchKernelGGL((attn_delta_kernel<64>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o), so,
+                         static_cast<const bf16_t*>(dout), sdo, delta, H, T, rows);
+    else
+      hipLaunchKernelGGL((attn_delta_kernel<128>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o),
+                         so, static_cast<const bf16_t*>(dout), sdo, delta, H, T, rows);
+    DAMD_CHECK_LAUNCH();
+  }
+  BwdArgs a;
+  a.q = static_cast<const bf16_t*>(q); a.k = static_cast<const bf16_t*>(k); a.v = static_cast<const bf16_t*>(v);
+  a.dout = static_cast<const bf16_t*>(dout); a.lse = lse; a.delta = delta; a.dq_acc = dq_acc;
+  a.dk = static_cast<bf16_t*>(dk); a.dv = static_cast<bf16_t*>(dv);
+  a.sq = sq; a.sk = sk; a.sv = sv; a.sdo = sdo; a.sdk = sdk; a.sdv = sdv;
+  a.H = H; a.T = T; a.scale = scale; a.scale_log2 = scale * kLog2e;
+  dim3 grid((T + kBlk - 1) / kBlk, H, B);
+  if (D == 64) {
+    const size_t sm = bwd_smem_bytes<64>();
+    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<64, true>), grid, dim3(kThreads), sm, st, a);
+    else hipLaunchKernelGGL((attn_bwd_kernel<64, false>), grid, dim3(kThreads), sm, st, a);
+  } else {
+    const size_t sm = bwd_smem_bytes<128>();
+    if (causal) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<128, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sm));
+      hipLaunchKernelGGL((attn_bwd_kernel<128, true>), grid, dim3(kThreads), sm, st, a);
+    } else {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<128, false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sm));
+      hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(kThreads), sm, st, a);
+    }
+  }
+  DAMD_CHECK_LAUNCH();
+  const int64_t n8 = rows * D / 8;
+  const int blocks = static_cast<int>((n8 + 255) / 256);
+  if (D == 64)
+    hipLaunchKernelGGL((attn_dq_convert_kernel<64>), dim3(blocks), dim3(256), 0, st, dq_acc,
+                       static_cast<bf16_t*>(dq), sdq, H, T, n8);
+  else
+    hipLaunchKernelGGL((attn_dq_convert_kernel<128>), dim3(blocks), dim3(256), 0, st, dq_acc,
+                       static_cast<bf16_t*>(dq), sdq, H, T, n8);
+  DAMD_CHECK_LAUNCH();
+}
+
+}  // extern "C"

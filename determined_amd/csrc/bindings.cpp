@@ -57,6 +57,12 @@ void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, co
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
                         const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
                         hipStream_t);
+// launchers (attention.hip)
+extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
+                                     int, int, float, int, hipStream_t);
+extern "C" void damd_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*,
+                                     float*, float*, void*, void*, void*, const int64_t*, int, int, int, int, float,
+                                     int, hipStream_t);
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -359,9 +365,84 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// ---------------------------------------------------------------- flash attention
+// q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
+// 16-byte aligned rows); D in {64, 128}; bf16.
+bool attn_supported(const at::Tensor& t) {
+  if (!t.is_cuda() || t.scalar_type() != at::kBFloat16 || t.dim() != 4) return false;
+  const int64_t D = t.size(3);
+  if (D != 64 && D != 128) return false;
+  if (t.stride(3) != 1) return false;
+  for (int i = 0; i < 3; ++i)
+    if (t.stride(i) % 8 != 0) return false;
+  return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0;
+}
+
+void check_attn(const at::Tensor& t, const at::Tensor& ref, const char* what) {
+  TORCH_CHECK(attn_supported(t), what, ": unsupported layout (need bf16 [B,H,T,D], D in {64,128}, contiguous D, "
+              "16-byte aligned strides)");
+  TORCH_CHECK(t.sizes() == ref.sizes(), what, " shape mismatch");
+}
+
+void push_strides(std::vector<int64_t>& s, const at::Tensor& t) {
+  s.push_back(t.stride(0));
+  s.push_back(t.stride(1));
+  s.push_back(t.stride(2));
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
+                                 double scale) {
+  check_attn(q, q, "q");
+  check_attn(k, q, "k");
+  check_attn(v, q, "v");
+  const int64_t B = q.size(0), H = q.size(1), T = q.size(2), D = q.size(3);
+  // output in [B, T, H, D] memory (so "merge heads" is a free view), returned as [B, H, T, D]
+  auto o = at::empty({B, T, H, D}, q.options()).permute({0, 2, 1, 3});
+  auto lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
+  std::vector<int64_t> s;
+  push_strides(s, q);
+  push_strides(s, k);
+  push_strides(s, v);
+  push_strides(s, o);
+  if (B * H * T > 0)
+    damd_attn_fwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), s.data(),
+                         static_cast<int>(B), static_cast<int>(H), static_cast<int>(T), static_cast<int>(D),
+                         static_cast<float>(scale), causal ? 1 : 0, cur_stream());
+  return {o, lse};
+}
+
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+              const at::Tensor& o, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, bool causal,
+              double scale) {
+  check_attn(q, q, "q");
+  check_attn(k, q, "k");
+  check_attn(v, q, "v");
+  check_attn(o, q, "o");
+  check_attn(dout, q, "dout");
+  check_attn(dq, q, "dq");
+  check_attn(dk, q, "dk");
+  check_attn(dv, q, "dv");
+  const int64_t B = q.size(0), H = q.size(1), T = q.size(2), D = q.size(3);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse [B,H,T] f32");
+  auto delta = at::empty({B, H, T}, lse.options());
+  auto dq_acc = at::empty({B, H, T, D}, lse.options());
+  std::vector<int64_t> s;
+  const at::Tensor* order[] = {&q, &k, &v, &o, &dout, &dk, &dv, &dq};
+  for (const at::Tensor* t : order) push_strides(s, *t);
+  if (B * H * T > 0)
+    damd_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                         lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(), dq.data_ptr(),
+                         dk.data_ptr(), dv.data_ptr(), s.data(), static_cast<int>(B), static_cast<int>(H),
+                         static_cast<int>(T), static_cast<int>(D), static_cast<float>(scale), causal ? 1 : 0,
+                         cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("attn_supported", &attn_supported);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);

@@ -9,8 +9,9 @@ tied input/output embedding, GELU-tanh MLP) laid out for MI355X:
 * bf16 weights and activations; LayerNorms are the wave-per-row fused HIP kernels
   (``ops.FusedLayerNorm``, ``csrc/norm.hip``);
 * QKV / output / MLP projections are plain ``[B*T, d] x [d, n]`` GEMMs (hipBLASLt, MFMA);
-* attention goes through ``ops.attention.causal_attention`` (flash attention, no [T, T]
-  score matrix in HBM);
+* attention is the hand-written MFMA flash-attention kernel (``ops.attention.qkv_attention``,
+  ``csrc/attention.hip``) on the packed QKV projection: no [T, T] score matrix in HBM and a
+  packed QKV gradient;
 * the vocabulary is padded to a multiple of 128 (50257 -> 50304) so the LM-head GEMM tiles
   evenly; padded logits are masked out of the loss;
 * optional activation checkpointing per block.
@@ -25,7 +26,7 @@ import torch.nn.functional as F
 from torch import nn
 from torch.utils.checkpoint import checkpoint
 
-from determined_amd.ops.attention import causal_attention
+from determined_amd.ops.attention import qkv_attention
 from determined_amd.ops.norm import FusedLayerNorm
 
 
@@ -36,7 +37,8 @@ class GPT2Config:
     n_embd: int = 1024
     n_layer: int = 24
     n_head: int = 16
-    dropout: float = 0.1
+    dropout: float = 0.1          # embedding / residual dropout
+    attn_dropout: float = 0.0     # attention-probability dropout (off, as in GPT-NeoX configs)
     layer_norm_epsilon: float = 1e-5
     pad_vocab_to: int = 128
     activation_checkpointing: bool = False
@@ -62,14 +64,15 @@ class CausalSelfAttention(nn.Module):
         self.n_head = cfg.n_head
         self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
-        self.dropout = cfg.dropout
+        self.attn_dropout = cfg.attn_dropout
         self.resid_drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, T, C = x.shape
         qkv = self.c_attn(x).view(B, T, 3, self.n_head, C // self.n_head)
-        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, D] each (strided views)
-        y = causal_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
+        # fused MFMA flash attention on the packed projection; returns [B, H, T, D] laid out
+        # as [B, T, H, D], so merging the heads below is a view
+        y = qkv_attention(qkv, causal=True, dropout_p=self.attn_dropout if self.training else 0.0)
         y = y.transpose(1, 2).reshape(B, T, C)
         return self.resid_drop(self.c_proj(y))
 
