@@ -63,6 +63,13 @@ extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void
 extern "C" void damd_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*,
                                      float*, float*, void*, void*, void*, const int64_t*, int, int, int, int, float,
                                      int, hipStream_t);
+// launchers (fused.hip)
+extern "C" void damd_lm_ce_fwd_launch(const void*, const int64_t*, int64_t, int, int, int, int64_t, float*, float*,
+                                      hipStream_t);
+extern "C" void damd_lm_ce_bwd_launch(const void*, const int64_t*, const float*, const float*, int64_t, int, int,
+                                      int, int64_t, void*, hipStream_t);
+extern "C" int damd_bias_grad_splits(int64_t, int);
+extern "C" void damd_bias_grad_launch(const void*, int64_t, int, int, float*, void*, int, hipStream_t);
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -437,9 +444,62 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
                          cur_stream());
 }
 
+// ---------------------------------------------------------------- fused LM loss / bias grad
+void check_lm(const at::Tensor& logits, const at::Tensor& labels) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.is_contiguous(),
+              "logits must be a contiguous bf16 GPU tensor [B, T, Vp]");
+  TORCH_CHECK(logits.dim() == 3 && logits.size(2) % 8 == 0, "logits must be [B, T, Vp] with Vp % 8 == 0");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.dim() == 2 &&
+                  labels.size(0) == logits.size(0) && labels.size(1) == logits.size(1),
+              "labels must be contiguous int64 [B, T]");
+}
+
+std::vector<at::Tensor> lm_ce_fwd(const at::Tensor& logits, const at::Tensor& labels, int64_t V,
+                                  int64_t ignore_index) {
+  check_lm(logits, labels);
+  const int64_t B = logits.size(0), T = logits.size(1), Vp = logits.size(2);
+  TORCH_CHECK(V > 0 && V <= Vp, "valid vocabulary must be in (0, Vp]");
+  auto opts = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({B, T}, opts);
+  auto lse = at::empty({B, T}, opts);
+  damd_lm_ce_fwd_launch(logits.data_ptr(), labels.data_ptr<int64_t>(), B * T, static_cast<int>(T),
+                        static_cast<int>(V), static_cast<int>(Vp), ignore_index, loss.data_ptr<float>(),
+                        lse.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+void lm_ce_bwd(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& scale,
+               int64_t V, int64_t ignore_index, at::Tensor& dlogits) {
+  check_lm(logits, labels);
+  TORCH_CHECK(dlogits.sizes() == logits.sizes() && dlogits.is_contiguous() &&
+                  dlogits.scalar_type() == at::kBFloat16, "dlogits must match logits");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == labels.numel(), "lse");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.is_cuda() && scale.numel() == 1, "scale: f32 scalar");
+  const int64_t B = logits.size(0), T = logits.size(1), Vp = logits.size(2);
+  damd_lm_ce_bwd_launch(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), scale.data_ptr<float>(),
+                        B * T, static_cast<int>(T), static_cast<int>(V), static_cast<int>(Vp), ignore_index,
+                        dlogits.data_ptr(), cur_stream());
+}
+
+at::Tensor bias_grad(const at::Tensor& g, at::ScalarType out_dtype) {
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kBFloat16 && g.is_contiguous(), "g: contiguous bf16 GPU tensor");
+  const int64_t N = g.size(-1), M = g.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(N % 8 == 0, "bias_grad needs N % 8 == 0");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "out dtype f32/bf16");
+  auto out = at::empty({N}, g.options().dtype(out_dtype));
+  const int splits = damd_bias_grad_splits(M, static_cast<int>(N));
+  auto part = at::empty({splits, N}, g.options().dtype(at::kFloat));
+  damd_bias_grad_launch(g.data_ptr(), M, static_cast<int>(N), splits, part.data_ptr<float>(), out.data_ptr(),
+                        out_dtype == at::kFloat ? 0 : 1, cur_stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("lm_ce_fwd", &lm_ce_fwd);
+  m.def("lm_ce_bwd", &lm_ce_bwd);
+  m.def("bias_grad", &bias_grad);
   m.def("attn_supported", &attn_supported);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

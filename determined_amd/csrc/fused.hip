@@ -1,0 +1,207 @@
+// Fused language-model head loss and elementwise helpers for gfx950.
+//
+// lm_ce: next-token cross-entropy straight from the bf16 LM-head GEMM output
+//   logits [B*T, Vp] (Vp = vocabulary padded for the GEMM, V = valid vocabulary),
+//   labels [B*T] (int64; the label of row (b, t) is labels[b, t+1], the last position of
+//   each sequence and label == ignore_index contribute nothing).
+//   forward: one workgroup per row, ONE pass over the row with an online (max, sum) per
+//            thread (16-byte loads), block merge -> row loss and log-sum-exp;
+//   backward: dlogits = (softmax - onehot) * (dloss / n_valid), written as bf16, optionally
+//            in place over the logits (they are dead after the loss), padded columns -> 0.
+//   Replaces: slice + reshape + bf16->fp32 copy + softmax fwd + softmax bwd + fills.
+//
+// bias_grad: column sums of a [M, N] bf16 gradient (the bias gradient of a Linear) with
+//   16-byte loads, row-split partials in fp32 and a second tiny pass.
+
+#include "common.h"
+
+#include <math.h>
+
+namespace damd {
+namespace fused {
+
+constexpr int kCEThreads = 256;
+
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+__global__ void __launch_bounds__(kCEThreads)
+lm_ce_fwd_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels, int T, int V, int Vp,
+                 int64_t ignore_index, float* __restrict__ row_loss, float* __restrict__ lse_out) {
+  const int64_t row = blockIdx.x;
+  const int t = static_cast<int>(row % T);
+  const bf16_t* x = logits + row * Vp;
+  int64_t lab = t + 1 < T ? labels[row + 1] : ignore_index;
+  if (lab == ignore_index || lab < 0 || lab >= V) lab = -1;
+  float m = -INFINITY, s = 0.f;
+  const int nvec = V / 8;
+  for (int i = threadIdx.x; i < nvec; i += kCEThreads) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    float f[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = bf2f(v.v[j]);
+      mx = fmaxf(mx, f[j]);
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(f[j] - mx);
+    online_merge(m, s, mx, ls);
+  }
+  for (int i = nvec * 8 + threadIdx.x; i < V; i += kCEThreads) online_merge(m, s, bf2f(x[i]), 1.f);
+  // wave merge
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+  __shared__ float sm[kCEThreads / 64], ss[kCEThreads / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[w] = m;
+    ss[w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int k = 1; k < kCEThreads / 64; ++k) online_merge(M, S, sm[k], ss[k]);
+    const float lse = M + logf(S);
+    lse_out[row] = lse;
+    row_loss[row] = lab >= 0 ? lse - bf2f(x[lab]) : 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(kCEThreads)
+lm_ce_bwd_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels, const float* __restrict__ lse,
+                 const float* __restrict__ scale_ptr, int T, int V, int Vp, int64_t ignore_index,
+                 bf16_t* __restrict__ dlogits) {
+  const int64_t row = blockIdx.x;
+  const int t = static_cast<int>(row % T);
+  int64_t lab = t + 1 < T ? labels[row + 1] : ignore_index;
+  const bool valid = !(lab == ignore_index || lab < 0 || lab >= V);
+  const bf16_t* x = logits + row * Vp;
+  bf16_t* dx = dlogits + row * Vp;
+  const float scale = valid ? *scale_ptr : 0.f;
+  const float L = lse[row];
+  const int nvec = Vp / 8;
+  for (int i = threadIdx.x; i < nvec; i += kCEThreads) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = i * 8 + j;
+      float g = 0.f;
+      if (col < V && scale != 0.f) {
+        g = __expf(bf2f(v.v[j]) - L);
+        if (col == lab) g -= 1.f;
+        g *= scale;
+      }
+      o.v[j] = f2bf(g);
+    }
+    *reinterpret_cast<bf16x8*>(dx + i * 8) = o;
+  }
+  for (int col = nvec * 8 + threadIdx.x; col < Vp; col += kCEThreads) {
+    float g = 0.f;
+    if (col < V && scale != 0.f) {
+      g = __expf(bf2f(x[col]) - L);
+      if (col == lab) g -= 1.f;
+      g *= scale;
+    }
+    dx[col] = f2bf(g);
+  }
+}
+
+// ---- bias gradient: out[n] = sum_m g[m, n] -----------------------------------------------
+constexpr int kBGCols = 512;  // columns per workgroup (64 lanes x 8)
+
+__global__ void __launch_bounds__(256)
+bias_grad_partial_kernel(const bf16_t* __restrict__ g, int64_t M, int N, int64_t rows_per_split,
+                         float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wr = threadIdx.x >> 6;
+  const int col = blockIdx.x * kBGCols + lane * 8;
+  const int64_t r0 = blockIdx.y * rows_per_split;
+  const int64_t r1 = min(M, r0 + rows_per_split);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+    for (int64_t r = r0 + wr; r < r1; r += 4) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + r * N + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v.v[j]);
+    }
+  }
+  __shared__ float red[4][kBGCols];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wr][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kBGCols; c += 256) {
+    const int gc = blockIdx.x * kBGCols + c;
+    if (gc < N) part[static_cast<int64_t>(blockIdx.y) * N + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
+}
+
+template <typename OT>
+__global__ void __launch_bounds__(256)
+bias_grad_finalize_kernel(const float* __restrict__ part, int splits, int N, OT* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[static_cast<int64_t>(k) * N + c];
+  Elem<OT>::st(out, c, s);
+}
+
+}  // namespace fused
+}  // namespace damd
+
+using namespace damd;
+using namespace damd::fused;
+
+extern "C" {
+
+void damd_lm_ce_fwd_launch(const void* logits, const int64_t* labels, int64_t rows, int T, int V, int Vp,
+                           int64_t ignore_index, float* row_loss, float* lse, hipStream_t st) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(lm_ce_fwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
+                     static_cast<const bf16_t*>(logits), labels, T, V, Vp, ignore_index, row_loss, lse);
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_lm_ce_bwd_launch(const void* logits, const int64_t* labels, const float* lse, const float* scale,
+                           int64_t rows, int T, int V, int Vp, int64_t ignore_index, void* dlogits, hipStream_t st) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(lm_ce_bwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
+                     static_cast<const bf16_t*>(logits), labels, lse, scale, T, V, Vp, ignore_index,
+                     static_cast<bf16_t*>(dlogits));
+  DAMD_CHECK_LAUNCH();
+}
+
+int damd_bias_grad_splits(int64_t M, int N) {
+  const int col_blocks = (N + kBGCols - 1) / kBGCols;
+  int splits = static_cast<int>((2048 + col_blocks - 1) / col_blocks);  // ~2048 workgroups
+  const int64_t max_splits = (M + 63) / 64;                             // >= 64 rows per split
+  if (splits > max_splits) splits = static_cast<int>(max_splits);
+  return splits < 1 ? 1 : splits;
+}
+
+void damd_bias_grad_launch(const void* g, int64_t M, int N, int splits, float* part, void* out, int out_dtype,
+                           hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  const int64_t rps = (M + splits - 1) / splits;
+  dim3 grid((N + kBGCols - 1) / kBGCols, splits);
+  hipLaunchKernelGGL(bias_grad_partial_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g), M, N, rps, part);
+  DAMD_CHECK_LAUNCH();
+  const dim3 g2((N + 255) / 256);
+  if (out_dtype == 0)
+    hipLaunchKernelGGL((bias_grad_finalize_kernel<float>), g2, dim3(256), 0, st, part, splits, N,
+                       static_cast<float*>(out));
+  else
+    hipLaunchKernelGGL((bias_grad_finalize_kernel<bf16_t>), g2, dim3(256), 0, st, part, splits, N,
+                       static_cast<bf16_t*>(out));
+  DAMD_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -27,6 +27,7 @@ from torch import nn
 from torch.utils.checkpoint import checkpoint
 
 from determined_amd.ops.attention import qkv_attention
+from determined_amd.ops.fused import FusedLinear, lm_cross_entropy
 from determined_amd.ops.norm import FusedLayerNorm
 
 
@@ -62,8 +63,8 @@ class CausalSelfAttention(nn.Module):
     def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
         self.n_head = cfg.n_head
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.c_attn = FusedLinear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = FusedLinear(cfg.n_embd, cfg.n_embd)
         self.attn_dropout = cfg.attn_dropout
         self.resid_drop = nn.Dropout(cfg.dropout)
 
@@ -80,8 +81,8 @@ class CausalSelfAttention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.c_fc = FusedLinear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = FusedLinear(4 * cfg.n_embd, cfg.n_embd)
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -153,9 +154,7 @@ class GPT2LMHeadModel(nn.Module):
 
 def lm_loss(logits: torch.Tensor, labels: torch.Tensor, vocab_size: int) -> torch.Tensor:
     """Shifted next-token cross-entropy in fp32 (``-100`` labels ignored, padded vocab masked)."""
-    lg = logits[:, :-1, :vocab_size].reshape(-1, vocab_size)
-    lg = lg.to(torch.promote_types(lg.dtype, torch.float32))
-    return F.cross_entropy(lg, labels[:, 1:].reshape(-1), ignore_index=-100)
+    return lm_cross_entropy(logits, labels, vocab_size, ignore_index=-100)
 
 
 def gpt2(name: str = "gpt2-medium", **overrides: Any) -> GPT2LMHeadModel:

@@ -80,3 +80,41 @@ def test_gpt2_block_uses_kernel():
     loss = m(x, labels=x)
     loss.backward()
     assert torch.isfinite(loss) and all(torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("V,Vp", [(50257, 50304), (512, 512), (1000, 1008)])
+def test_lm_cross_entropy_matches_reference(V, Vp):
+    from determined_amd.ops.fused import lm_cross_entropy
+
+    torch.manual_seed(3)
+    B, T = 2, 37
+    base = (torch.randn(B, T, Vp, device="cuda") * 3).bfloat16()
+    labels = torch.randint(0, V, (B, T), device="cuda")
+    labels[0, 5] = -100
+    lg = base.clone().requires_grad_(True)
+    loss = lm_cross_entropy(lg, labels, V)
+    loss.backward()
+    ref = base.float().clone().requires_grad_(True)
+    rl = torch.nn.functional.cross_entropy(ref[:, :-1, :V].reshape(-1, V), labels[:, 1:].reshape(-1),
+                                           ignore_index=-100)
+    rl.backward()
+    torch.testing.assert_close(loss.float(), rl, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(lg.grad.float(), ref.grad, rtol=2e-2, atol=1e-4)
+
+
+def test_fused_linear_bias_grad():
+    from determined_amd.ops.fused import FusedLinear
+
+    torch.manual_seed(4)
+    lin = FusedLinear(64, 96).cuda().bfloat16()
+    ref = torch.nn.Linear(64, 96).cuda().float()
+    ref.load_state_dict({k: v.float() for k, v in lin.state_dict().items()})
+    x = torch.randn(4, 33, 64, device="cuda").bfloat16()
+    xr = x.float().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    dy = torch.randn(4, 33, 96, device="cuda").bfloat16()
+    lin(xb).backward(dy)
+    ref(xr).backward(dy.float())
+    torch.testing.assert_close(lin.bias.grad.float(), ref.bias.grad, rtol=1e-2, atol=5e-2)
+    torch.testing.assert_close(lin.weight.grad.float(), ref.weight.grad, rtol=2e-2, atol=1e-1)
+    torch.testing.assert_close(xb.grad.float(), xr.grad, rtol=2e-2, atol=5e-2)
