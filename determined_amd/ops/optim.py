@@ -36,7 +36,7 @@ def _dcode(t: torch.Tensor) -> int:
 
 
 class _Plan:
-    __slots__ = ("key", "table", "n_chunks", "p_dtype", "g_dtype", "has_lp", "groups")
+    __slots__ = ("key", "table", "n_chunks", "p_dtype", "g_dtype", "has_lp", "groups", "wvec")
 
     def __init__(self, key, table, n_chunks, p_dtype, g_dtype, has_lp, groups):
         self.key = key
@@ -46,6 +46,7 @@ class _Plan:
         self.g_dtype = g_dtype
         self.has_lp = has_lp
         self.groups = groups
+        self.wvec = None
 
 
 def _ptrs(ts: List[torch.Tensor]) -> Tuple[int, ...]:
@@ -84,6 +85,9 @@ class _FusedBase(torch.optim.Optimizer):
         self.last_grad_norm: Optional[torch.Tensor] = None
         # set by sharded engines (ZeRO): all-reduces the local sum of squared grads in place
         self._partial_reducer: Optional[Callable[[torch.Tensor], None]] = None
+        # optional per-parameter weight of its squared-gradient contribution to the global
+        # norm (tensor parallelism: replicated params count 1/tp on each TP rank)
+        self._norm_weight: Optional[Callable[[torch.Tensor], float]] = None
 
     # -- step counter --------------------------------------------------------------------
     def _step_tensor(self, device: torch.device) -> torch.Tensor:
@@ -162,6 +166,13 @@ class _FusedBase(torch.optim.Optimizer):
                 if g.stride() != p.stride() or not is_dense(g):
                     raise RuntimeError("fused optimizers require dense grads laid out like their params")
             plan = _build_plan(b["p"], b["g"], b["s0"], b["s1"], b["lp"], b["grp"], ck)
+            plan.wvec = None
+            if self._norm_weight is not None:
+                ws = []
+                for lp_t, t in zip(b["lp"] or b["p"], b["p"]):
+                    ws += [float(self._norm_weight(lp_t))] * ((t.numel() + CHUNK - 1) // CHUNK)
+                if any(w != 1.0 for w in ws):
+                    plan.wvec = torch.tensor(ws, dtype=torch.float32, device=b["p"][0].device)
             self._plans[key] = plan
         return plan
 
@@ -218,9 +229,14 @@ class _FusedBase(torch.optim.Optimizer):
                     off += pl.n_chunks
                 fi = found_inf if found_inf is not None else aux["found_inf"]
                 partial, n_partial = aux["partial"], total
+                if any(pl.wvec is not None for _, pl in plans):
+                    ws = torch.cat([pl.wvec if pl.wvec is not None else
+                                    torch.ones(pl.n_chunks, dtype=torch.float32, device=dev) for _, pl in plans])
+                    partial = (aux["partial"][:total] * ws).sum(0, keepdim=True)
+                    n_partial = 1
                 if self._partial_reducer is not None:
                     # sharded optimizer: combine this shard's sum of squares across ranks
-                    partial = aux["partial"][:total].sum(0, keepdim=True)
+                    partial = partial[:n_partial].sum(0, keepdim=True)
                     self._partial_reducer(partial)
                     n_partial = 1
                 # finalize: clip coefficient x inv loss scale, found_inf, and the device
@@ -249,7 +265,8 @@ class _FusedBase(torch.optim.Optimizer):
         if self.max_grad_norm is not None and (params or self._partial_reducer is not None):
             sq = torch.zeros(1, dtype=torch.float32)
             for p in params:
-                sq += (p.grad.float() ** 2).sum()
+                w = float(self._norm_weight(p)) if self._norm_weight is not None else 1.0
+                sq += (p.grad.float() ** 2).sum() * w
             if self._partial_reducer is not None:
                 self._partial_reducer(sq)
             norm = torch.sqrt(sq[0]) * gscale

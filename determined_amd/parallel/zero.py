@@ -592,6 +592,12 @@ class ZeroEngine(nn.Module):
         if mpu is not None and hasattr(mpu, "get_data_parallel_group"):
             process_group = mpu.get_data_parallel_group()
         self.process_group = process_group
+        # tensor/model parallelism: gradients are reduced over the data-parallel group only;
+        # the clipping norm additionally sums over the model-parallel group
+        self.mp_group = mpu.get_model_parallel_group() if mpu is not None and \
+            hasattr(mpu, "get_model_parallel_group") else None
+        self.mp_size = int(mpu.get_model_parallel_world_size()) if mpu is not None and \
+            hasattr(mpu, "get_model_parallel_world_size") else 1
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size(process_group) if self.distributed else 1
         self.global_rank = dist.get_rank() if self.distributed else 0
@@ -691,7 +697,16 @@ class ZeroEngine(nn.Module):
                     info_groups[gi].append((self._pindex[id(p)], s, e))
         self.optimizer._bind(frag_groups, [fi for grp in info_groups for fi in grp])
         if self.optimizer.inner is not None and hasattr(self.optimizer.inner, "_partial_reducer"):
-            self.optimizer.inner._partial_reducer = self._allreduce_norm if self._shard_world > 1 else None
+            inner = self.optimizer.inner
+            inner._partial_reducer = self._allreduce_norm if (self._shard_world > 1 or self.mp_size > 1) else None
+            if self.mp_size > 1:
+                # each TP rank holds different shards of sharded params but a full copy of
+                # replicated ones: count the latter 1/tp per rank so the TP sum counts them once
+                wmap = {}
+                for frag, (pi, _, _) in zip(self.optimizer._inner_params(), self.optimizer.frag_info):
+                    sharded = bool(getattr(self._params[pi], "tensor_model_parallel", False))
+                    wmap[id(frag)] = 1.0 if sharded else 1.0 / self.mp_size
+                inner._norm_weight = lambda t, _w=wmap: _w.get(id(t), 1.0)
         if config.gradient_clipping > 0 and self.optimizer.inner is not None:
             if hasattr(self.optimizer.inner, "set_grad_clipping"):
                 self.optimizer.inner.set_grad_clipping(config.gradient_clipping)
@@ -725,7 +740,10 @@ class ZeroEngine(nn.Module):
                     off += t.numel()
 
     def _allreduce_norm(self, sumsq: torch.Tensor) -> None:
-        dist.all_reduce(sumsq, group=self.process_group)
+        if self._shard_world > 1:
+            dist.all_reduce(sumsq, group=self.process_group)
+        if self.mp_size > 1:
+            dist.all_reduce(sumsq, group=self.mp_group)
 
     # -- gradient hooks -------------------------------------------------------------------------
     def _make_hook(self, p: nn.Parameter) -> Callable[[torch.Tensor], None]:
@@ -873,7 +891,7 @@ class ZeroEngine(nn.Module):
                 self._clip_generic(inner)
             inner.step()
             self._grad_norm = getattr(inner, "last_grad_norm", None)
-        elif self.config.gradient_clipping > 0 and self._shard_world > 1:
+        elif self.config.gradient_clipping > 0 and (self._shard_world > 1 or self.mp_size > 1):
             self._allreduce_norm(torch.zeros(1, dtype=torch.float32, device=self.device))
         self._gather()
         # Stream-level wait (RCCL): later kernels on the compute stream see the gathered
