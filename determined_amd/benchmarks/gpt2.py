@@ -28,7 +28,13 @@ def main() -> None:
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
     ap.add_argument("--bucket", type=int, default=16 * 1024 * 1024)
+    ap.add_argument("--tunable", default="", help="enable PyTorch TunableOp GEMM tuning; results file path")
     a = ap.parse_args()
+    if a.tunable:
+        # hipBLASLt/rocBLAS solution search per GEMM shape (done during warm-up, cached in a file)
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(a.tunable)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

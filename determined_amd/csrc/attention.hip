@@ -1,25 +1,28 @@
 // Flash attention (forward + backward) for gfx950 / MI355X: bf16 in/out, fp32 accumulate,
 // online softmax, optional causal mask, head dim D in {64, 128}.
 //
-// MFMA: v_mfma_f32_16x16x32_bf16 (64-wide wave computes a 16x16 tile, K = 32).
+// MFMA: v_mfma_f32_16x16x32_bf16 (a 64-wide wave computes a 16x16 tile, K = 32).
 //   A operand: lane l holds A[row l&15][k 8(l>>4)+j], B operand: B[k 8(l>>4)+j][col l&15],
 //   C/D: C[row 4(l>>4)+r][col l&15], r = 0..3.
+// Transposed operands come from the SAME row-major LDS tile through ds_read_b64_tr_b16
+// (gfx950 hardware transpose read: per 16-lane group, lane 4q+p addresses row q, columns
+// 4p..4p+3 of a 4x16 block and lane i receives column i of the 4 rows).
 //
-// Forward (one workgroup = 4 waves = 64 query rows, a wave = 16 rows):
-//   S^T = K.Q^T so the query sits on the lane (col) and 4 keys per 16-key tile sit in the
-//   lane's registers: the row max / row sum of the online softmax are in-lane + 2 xor
-//   shuffles, the running (m, l) and the rescale of O are lane-local, and O^T = V^T.P^T takes
-//   P^T straight from the S^T accumulators (no LDS round trip): a 32-key MFMA step permutes
-//   its k index as key(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4), and the V^T operand is read
-//   in that same order from a transposed LDS image Vt[d][key].
-//   K/V tiles (64 keys) are staged once per workgroup in LDS and shared by the 4 waves.
+// Forward (workgroup = 4 waves = 128 query rows, a wave = 2 x 16 rows):
+//   S^T = K.Q^T puts the query on the lane (col) and 4 keys per 16-key tile in the lane's
+//   registers: the online-softmax row max / sum are in-lane + 2 xor shuffles, the running
+//   (m, l) and the rescale of O are lane-local, and O^T = V^T.P^T consumes P^T straight from
+//   the S^T accumulators: a 32-key MFMA step uses the k order key(g, j) = (j < 4 ? 4g + j :
+//   16 + 4g + j - 4), and the V^T operand is read in that order with two transposed reads.
+//   K/V tiles (64 keys) are staged in LDS once per workgroup; the next tile's global loads
+//   are issued into registers before the current tile's MFMAs (latency hidden).
 //
-// Backward (one workgroup = 64 keys, a wave = 16 keys; loop over 64-row query blocks):
-//   S = Q.K^T and dP = dO.V^T with the key on the lane (K, V fragments of the wave's own keys
-//   stay in registers), P = exp2(S.scale.log2e - LSE.log2e), dS = P.(dP - delta); the
-//   accumulators feed dV^T = dO^T.P and dK^T = Q^T.dS directly (same k permutation, Q^T/dO^T
-//   from transposed LDS images); dS goes through LDS once for dQ = dS.K, which is added into
-//   an fp32 buffer with float atomics and converted to bf16 by a final pass.
+// Backward (workgroup = 64 keys, a wave = 16 keys; loop over 64-row query blocks):
+//   S = Q.K^T and dP = dO.V^T with the key on the lane (K, V fragments of the wave's keys stay
+//   in registers), P = exp2(S.scale.log2e - LSE.log2e), dS = P.(dP - delta); P / dS feed
+//   dV^T = dO^T.P and dK^T = Q^T.dS directly (dO^T, Q^T by transposed reads of the row-major
+//   tiles); dS crosses LDS once for dQ = dS.K, summed into an fp32 buffer with float atomics
+//   and converted to bf16 by a final pass.
 //
 // Strides are in elements for (batch, head, token); the head dimension must be contiguous.
 
@@ -34,9 +37,12 @@ typedef short s8 __attribute__((ext_vector_type(8)));
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
 
-constexpr int kBlk = 64;       // query rows per fwd workgroup == keys per bwd workgroup == kv tile
+constexpr int kBlk = 64;       // kv tile (fwd) / key block (bwd) / query block (bwd)
 constexpr int kThreads = 256;  // 4 waves
+constexpr int kQT = 2;         // 16-row query tiles per wave in the forward
+constexpr int kFwdRows = 4 * 16 * kQT;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -65,7 +71,14 @@ __device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
 
 __device__ __forceinline__ short bfs(float x) { return static_cast<short>(f2bf(x)); }
 
-// P^T / dS fragment of a 32-key (or 32-query) k step from two 16-wide accumulator tiles.
+__device__ __forceinline__ s8 cat4(s4 lo, s4 hi) {
+  s8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// bf16 fragment from two 16-wide accumulator tiles (the permuted 32-wide k step).
 __device__ __forceinline__ s8 pack_pair(f4 lo, f4 hi) {
   s8 r;
   r[0] = bfs(lo[0]); r[1] = bfs(lo[1]); r[2] = bfs(lo[2]); r[3] = bfs(lo[3]);
@@ -73,141 +86,180 @@ __device__ __forceinline__ s8 pack_pair(f4 lo, f4 hi) {
   return r;
 }
 
-// Operand read in the permuted k order from a transposed image row: keys 4g..4g+3 and
-// 16+4g..16+4g+3 of the 32-wide step starting at `row`.
-__device__ __forceinline__ s8 read_perm(const bf16_t* row, int g) {
-  const s4 lo = *reinterpret_cast<const s4*>(row + 4 * g);
-  const s4 hi = *reinterpret_cast<const s4*>(row + 16 + 4 * g);
-  s8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
+__device__ __forceinline__ s4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p));
 }
 
-// Cooperative 64 x D tile load: row-major image (row stride D+8) and/or transposed image
-// (row stride 64+8).  Rows >= T are zero.
-template <int D, bool ROW, bool TRANS>
-__device__ __forceinline__ void load_tile(const bf16_t* __restrict__ base, int64_t st, int r0, int T,
-                                          bf16_t* rowimg, bf16_t* trimg) {
-  constexpr int CH = D / 8;
-  for (int i = threadIdx.x; i < kBlk * CH; i += kThreads) {
-    const int r = i / CH, c = (i % CH) * 8;
-    s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r0 + r < T) x = *reinterpret_cast<const s8*>(base + static_cast<int64_t>(r0 + r) * st + c);
-    if (ROW) *reinterpret_cast<s8*>(rowimg + r * (D + 8) + c) = x;
-    if (TRANS) {
+// Transposed operand (rows of the image are the k index): lane c of each 16-lane group gets
+// column col0 + c of image rows {r0 + q} (elements 0..3) and {r1 + q} (elements 4..7).
+__device__ __forceinline__ s8 tr_pair(const bf16_t* img, int stride, int r0, int r1, int col0, int c) {
+  const int q = c >> 2, p = c & 3;
+  const s4 lo = tr_read(img + (r0 + q) * stride + col0 + 4 * p);
+  const s4 hi = tr_read(img + (r1 + q) * stride + col0 + 4 * p);
+  return cat4(lo, hi);
+}
+
+// Register-staged tile of `ROWS` x D bf16: global -> registers (issued early), registers ->
+// row-major LDS image (row stride D + 8).  Rows >= T load zeros.
+template <int D, int ROWS>
+struct Stage {
+  static constexpr int CH = D / 8;
+  static constexpr int N = ROWS * CH / kThreads;
+  s8 r[N];
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, int64_t st, int r0, int T) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) trimg[(c + j) * (kBlk + 8) + r] = x[j];
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + i * kThreads, row = idx / CH, col = (idx % CH) * 8;
+      s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (r0 + row < T) x = *reinterpret_cast<const s8*>(base + static_cast<int64_t>(r0 + row) * st + col);
+      r[i] = x;
     }
   }
-}
+  __device__ __forceinline__ void store(bf16_t* img) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + i * kThreads, row = idx / CH, col = (idx % CH) * 8;
+      *reinterpret_cast<s8*>(img + row * (D + 8) + col) = r[i];
+    }
+  }
+};
 
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
-  constexpr int KP = D + 8, VP = kBlk + 8;
+  constexpr int KP = D + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[D * VP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[kBlk * KP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int T = a.T, nblk = (T + kBlk - 1) / kBlk;
-  const int qb = CAUSAL ? (nblk - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
+  const int T = a.T, nkb = (T + kBlk - 1) / kBlk, nqb = (T + kFwdRows - 1) / kFwdRows;
+  const int qb = CAUSAL ? (nqb - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
   const int h = blockIdx.y, b = blockIdx.z;
-  const int q0 = qb * kBlk;
+  const int q0 = qb * kFwdRows, qw = q0 + w * 16 * kQT;  // first query row of this wave
   const bf16_t* Qp = a.q + b * a.sq.b + h * a.sq.h;
   const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
   const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
-  const int myq = q0 + w * 16 + c;  // query whose softmax state this lane carries
 
-  s8 qf[D / 32];
+  s8 qf[kQT][D / 32];
 #pragma unroll
-  for (int ds = 0; ds < D / 32; ++ds) {
-    s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (myq < T) x = *reinterpret_cast<const s8*>(Qp + static_cast<int64_t>(myq) * a.sq.t + ds * 32 + 8 * g);
-    qf[ds] = x;
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int q = qw + qt * 16 + c;
+#pragma unroll
+    for (int ds = 0; ds < D / 32; ++ds) {
+      s8 x = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (q < T) x = *reinterpret_cast<const s8*>(Qp + static_cast<int64_t>(q) * a.sq.t + ds * 32 + 8 * g);
+      qf[qt][ds] = x;
+    }
   }
-  f4 oacc[D / 16];
+  f4 oacc[kQT][D / 16];
+  float m[kQT], l[kQT];
 #pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) oacc[dt] = f4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int qt = 0; qt < kQT; ++qt) {
+    m[qt] = -INFINITY;
+    l[qt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) oacc[qt][dt] = f4{0.f, 0.f, 0.f, 0.f};
+  }
 
-  const int kb_end = CAUSAL ? min(nblk, (q0 + kBlk - 1) / kBlk + 1) : nblk;
+  const int kb_end = CAUSAL ? min(nkb, (q0 + kFwdRows - 1) / kBlk + 1) : nkb;
+  Stage<D, kBlk> ks, vs;
+  ks.load(Kp, a.sk.t, 0, T);
+  vs.load(Vp, a.sv.t, 0, T);
   for (int kb = 0; kb < kb_end; ++kb) {
     const int k0 = kb * kBlk;
     __syncthreads();
-    load_tile<D, true, false>(Kp, a.sk.t, k0, T, Ks, nullptr);
-    load_tile<D, false, true>(Vp, a.sv.t, k0, T, nullptr, Vt);
+    ks.store(Ks);
+    vs.store(Vs);
     __syncthreads();
-
-    f4 s[4];
+    if (kb + 1 < kb_end) {  // next tile's loads fly under this tile's MFMAs
+      ks.load(Kp, a.sk.t, k0 + kBlk, T);
+      vs.load(Vp, a.sv.t, k0 + kBlk, T);
+    }
+    f4 s[kQT][4];
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) s[qt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      s[nt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ds = 0; ds < D / 32; ++ds) {
         const s8 kf = *reinterpret_cast<const s8*>(Ks + (nt * 16 + c) * KP + ds * 32 + 8 * g);
-        s[nt] = mfma(kf, qf[ds], s[nt]);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt) s[qt][nt] = mfma(kf, qf[qt][ds], s[qt][nt]);
       }
     }
-    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && k0 + kBlk - 1 > q0 + w * 16);
-    float mx = -INFINITY;
+    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && k0 + kBlk - 1 > qw);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int qt = 0; qt < kQT; ++qt) {
+      const int myq = qw + qt * 16 + c;
+      float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = s[nt][r] * a.scale_log2;
-        if (need_mask) {
-          const int key = k0 + nt * 16 + 4 * g + r;
-          if (key >= T || (CAUSAL && key > myq)) v = -INFINITY;
+      for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = s[qt][nt][r] * a.scale_log2;
+          if (need_mask) {
+            const int key = k0 + nt * 16 + 4 * g + r;
+            if (key >= T || (CAUSAL && key > myq)) v = -INFINITY;
+          }
+          s[qt][nt][r] = v;
+          mx = fmaxf(mx, v);
         }
-        s[nt][r] = v;
-        mx = fmaxf(mx, v);
       }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m - m_use);
-    float rs = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m[qt], mx);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = exp2f(m[qt] - m_use);
+      float rs = 0.f;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[nt][r] - m_use);
-        s[nt][r] = p;
-        rs += p;
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[qt][nt][r] - m_use);
+          s[qt][nt][r] = p;
+          rs += p;
+        }
       }
-    }
-    l = l * alpha + rs;
-    m = m_new;
+      l[qt] = l[qt] * alpha + rs;
+      m[qt] = m_new;
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) oacc[dt] *= alpha;
+      for (int dt = 0; dt < D / 16; ++dt) oacc[qt][dt] *= alpha;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const s8 pb = pack_pair(s[2 * s2], s[2 * s2 + 1]);
+      s8 pb[kQT];
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) pb[qt] = pack_pair(s[qt][2 * s2], s[qt][2 * s2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
-        const s8 vf = read_perm(Vt + (dt * 16 + c) * VP + s2 * 32, g);
-        oacc[dt] = mfma(vf, pb, oacc[dt]);
+        const s8 vf = tr_pair(Vs, KP, s2 * 32 + 4 * g, s2 * 32 + 16 + 4 * g, dt * 16, c);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt) oacc[qt][dt] = mfma(vf, pb[qt], oacc[qt][dt]);
       }
     }
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (myq < T) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    bf16_t* Op = a.o + b * a.so.b + h * a.so.h + static_cast<int64_t>(myq) * a.so.t;
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      s4 ov;
+  for (int qt = 0; qt < kQT; ++qt) {
+    float lt = l[qt];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int myq = qw + qt * 16 + c;
+    if (myq < T) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16_t* Op = a.o + b * a.so.b + h * a.so.h + static_cast<int64_t>(myq) * a.so.t;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ov[r] = bfs(oacc[dt][r] * inv);
-      *reinterpret_cast<s4*>(Op + dt * 16 + 4 * g) = ov;
+      for (int dt = 0; dt < D / 16; ++dt) {
+        s4 ov;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = bfs(oacc[qt][dt][r] * inv);
+        *reinterpret_cast<s4*>(Op + dt * 16 + 4 * g) = ov;
+      }
+      if (g == 0)
+        a.lse[(static_cast<int64_t>(b) * a.H + h) * T + myq] = lt > 0.f ? m[qt] * kLn2 + logf(lt) : -INFINITY;
     }
-    if (g == 0)
-      a.lse[(static_cast<int64_t>(b) * a.H + h) * T + myq] = l > 0.f ? m * kLn2 + logf(l) : -INFINITY;
   }
 }
 
@@ -239,16 +291,12 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
-  constexpr int RP = D + 8, TP = kBlk + 8;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem_raw);  // [64][RP]
-  bf16_t* dOs = Qs + kBlk * RP;                       // [64][RP]
-  bf16_t* Qt = dOs + kBlk * RP;                       // [D][TP]
-  bf16_t* dOt = Qt + D * TP;                          // [D][TP]
-  bf16_t* Kt = dOt + D * TP;                          // [D][TP]  (this workgroup's keys)
-  bf16_t* dSs = Kt + D * TP;                          // [64 q][TP]
-  float* lse2 = reinterpret_cast<float*>(dSs + kBlk * TP);  // [64]
-  float* dl = lse2 + kBlk;                                  // [64]
+  constexpr int RP = D + 8, SP = kBlk + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[kBlk * RP];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[kBlk * RP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * RP];  // this workgroup's keys
+  __shared__ __attribute__((aligned(16))) bf16_t dSs[kBlk * SP];  // [q][key]
+  __shared__ float lse2[kBlk], dl[kBlk];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int T = a.T, nblk = (T + kBlk - 1) / kBlk;
@@ -272,22 +320,34 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
     kf[ds] = x;
     vf[ds] = y;
   }
-  load_tile<D, false, true>(Kp, a.sk.t, k0, T, nullptr, Kt);
+  {
+    Stage<D, kBlk> kst;
+    kst.load(Kp, a.sk.t, k0, T);
+    kst.store(Ks);
+  }
   f4 dk[D / 16], dv[D / 16];
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) dk[dt] = dv[dt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int qb = CAUSAL ? kb : 0; qb < nblk; ++qb) {
+  const int qb0 = CAUSAL ? kb : 0;
+  Stage<D, kBlk> qst, ost;
+  qst.load(Qp, a.sq.t, qb0 * kBlk, T);
+  ost.load(dOp, a.sdo.t, qb0 * kBlk, T);
+  for (int qb = qb0; qb < nblk; ++qb) {
     const int q0 = qb * kBlk;
     __syncthreads();
-    load_tile<D, true, true>(Qp, a.sq.t, q0, T, Qs, Qt);
-    load_tile<D, true, true>(dOp, a.sdo.t, q0, T, dOs, dOt);
+    qst.store(Qs);
+    ost.store(dOs);
     if (threadIdx.x < kBlk) {
       const int q = q0 + threadIdx.x;
       lse2[threadIdx.x] = q < T ? a.lse[bh * T + q] * kLog2e : INFINITY;
       dl[threadIdx.x] = q < T ? a.delta[bh * T + q] : 0.f;
     }
     __syncthreads();
+    if (qb + 1 < nblk) {
+      qst.load(Qp, a.sq.t, q0 + kBlk, T);
+      ost.load(dOp, a.sdo.t, q0 + kBlk, T);
+    }
 
     const bool need_mask = (k0 + kBlk > T) || (CAUSAL && q0 < k0 + kBlk);
     f4 P[4], dS[4];
@@ -317,15 +377,15 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
       const s8 sb = pack_pair(dS[2 * s2], dS[2 * s2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
-        dv[dt] = mfma(read_perm(dOt + (dt * 16 + c) * TP + s2 * 32, g), pb, dv[dt]);
-        dk[dt] = mfma(read_perm(Qt + (dt * 16 + c) * TP + s2 * 32, g), sb, dk[dt]);
+        dv[dt] = mfma(tr_pair(dOs, RP, s2 * 32 + 4 * g, s2 * 32 + 16 + 4 * g, dt * 16, c), pb, dv[dt]);
+        dk[dt] = mfma(tr_pair(Qs, RP, s2 * 32 + 4 * g, s2 * 32 + 16 + 4 * g, dt * 16, c), sb, dk[dt]);
       }
     }
     // dS -> LDS [q][key] for dQ = dS . K
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dSs[(qt * 16 + 4 * g + r) * TP + w * 16 + c] = static_cast<bf16_t>(bfs(dS[qt][r]));
+      for (int r = 0; r < 4; ++r) dSs[(qt * 16 + 4 * g + r) * SP + w * 16 + c] = static_cast<bf16_t>(bfs(dS[qt][r]));
     }
     __syncthreads();
     f4 dq[D / 16];
@@ -333,10 +393,11 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
     for (int dt = 0; dt < D / 16; ++dt) dq[dt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const s8 sa = *reinterpret_cast<const s8*>(dSs + (w * 16 + c) * TP + ks * 32 + 8 * g);
+      const s8 sa = *reinterpret_cast<const s8*>(dSs + (w * 16 + c) * SP + ks * 32 + 8 * g);
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
-        const s8 kt = *reinterpret_cast<const s8*>(Kt + (dt * 16 + c) * TP + ks * 32 + 8 * g);
+        // B = K[key = ks*32 + 8g + j][d = dt*16 + c]: natural k order, two transposed reads
+        const s8 kt = tr_pair(Ks, RP, ks * 32 + 8 * g, ks * 32 + 8 * g + 4, dt * 16, c);
         dq[dt] = mfma(sa, kt, dq[dt]);
       }
     }
@@ -387,11 +448,6 @@ __global__ void __launch_bounds__(256) attn_dq_convert_kernel(const float* __res
   *reinterpret_cast<s8*>(dq + b * s.b + h * s.h + t * s.t + d) = o;
 }
 
-template <int D>
-constexpr size_t bwd_smem_bytes() {
-  return sizeof(bf16_t) * (2 * kBlk * (D + 8) + 3 * D * (kBlk + 8) + kBlk * (kBlk + 8)) + 2 * kBlk * sizeof(float);
-}
-
 }  // namespace attn
 }  // namespace damd
 
@@ -409,7 +465,7 @@ void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   a.sq = {strides[0], strides[1], strides[2]}; a.sk = {strides[3], strides[4], strides[5]};
   a.sv = {strides[6], strides[7], strides[8]}; a.so = {strides[9], strides[10], strides[11]};
   a.H = H; a.T = T; a.scale_log2 = scale * kLog2e;
-  dim3 grid((T + kBlk - 1) / kBlk, H, B);
+  dim3 grid((T + kFwdRows - 1) / kFwdRows, H, B);
   if (D == 64) {
     if (causal) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
@@ -420,7 +476,7 @@ void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   DAMD_CHECK_LAUNCH();
 }
 
-// strides: 7 tensors (q, k, v, o, dout, dk, dv) + dq  (8 x 3)
+// strides: 8 tensors (q, k, v, o, dout, dk, dv, dq) x (b, h, t)
 void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                           const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
                           const int64_t* s, int B, int H, int T, int D, float scale, int causal, hipStream_t st) {
@@ -447,20 +503,11 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   a.H = H; a.T = T; a.scale = scale; a.scale_log2 = scale * kLog2e;
   dim3 grid((T + kBlk - 1) / kBlk, H, B);
   if (D == 64) {
-    const size_t sm = bwd_smem_bytes<64>();
-    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<64, true>), grid, dim3(kThreads), sm, st, a);
-    else hipLaunchKernelGGL((attn_bwd_kernel<64, false>), grid, dim3(kThreads), sm, st, a);
+    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
   } else {
-    const size_t sm = bwd_smem_bytes<128>();
-    if (causal) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<128, true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sm));
-      hipLaunchKernelGGL((attn_bwd_kernel<128, true>), grid, dim3(kThreads), sm, st, a);
-    } else {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<128, false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sm));
-      hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(kThreads), sm, st, a);
-    }
+    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
   }
   DAMD_CHECK_LAUNCH();
   const int64_t n8 = rows * D / 8;

@@ -45,8 +45,9 @@ void damd_scale_launch(const void*, int, const float*, int, hipStream_t);
 void damd_norm_fwd_launch(const void*, const void*, const void*, void*, float*, float*, int64_t, int, float,
                           int, int, int, hipStream_t);
 int damd_norm_bwd_blocks(int64_t);
-void damd_norm_bwd_launch(const void*, const void*, const float*, const float*, const void*, void*, float*,
-                          float*, int64_t, int, int, int, int, hipStream_t);
+int damd_norm_bwd_launch(const void*, const void*, const float*, const float*, const void*, void*, float*,
+                         float*, int64_t, int, int, int, int, hipStream_t);
+void damd_norm_wgrad_finalize_launch(const float*, const float*, int, int, void*, void*, int, hipStream_t);
 void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
@@ -250,20 +251,23 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, cons
   const int64_t rows = x.numel() / H;
   auto dx = at::empty_like(x);
   auto fopts = x.options().dtype(at::kFloat);
-  auto dgamma = at::zeros({H}, fopts);
-  auto dbeta = rms ? at::empty({0}, fopts) : at::zeros({H}, fopts);
+  // weight gradients come out in the weight dtype: per-block partials + one finalize pass
+  auto dgamma = at::empty({H}, gamma.options());
+  auto dbeta = rms ? at::empty({0}, gamma.options()) : at::empty({H}, gamma.options());
   if (rows > 0) {
-    const int W = damd_norm_bwd_blocks(rows) * 4;
-    auto part_g = at::empty({W, H}, fopts);
-    auto part_b = rms ? at::empty({0}, fopts) : at::empty({W, H}, fopts);
-    damd_norm_bwd_launch(dy.data_ptr(), x.data_ptr(), rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         gamma.data_ptr(), dx.data_ptr(), part_g.data_ptr<float>(),
-                         rms ? nullptr : part_b.data_ptr<float>(), rows, static_cast<int>(H), rms, dtype_code(x),
-                         dtype_code(gamma), cur_stream());
-    damd_col_reduce_launch(part_g.data_ptr<float>(), dgamma.data_ptr<float>(), W, static_cast<int>(H), cur_stream());
-    if (!rms)
-      damd_col_reduce_launch(part_b.data_ptr<float>(), dbeta.data_ptr<float>(), W, static_cast<int>(H),
-                             cur_stream());
+    const int cap = damd_norm_bwd_blocks(rows) * 4;
+    auto part_g = at::empty({cap, H}, fopts);
+    auto part_b = rms ? at::empty({0}, fopts) : at::empty({cap, H}, fopts);
+    const int W = damd_norm_bwd_launch(dy.data_ptr(), x.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
+                                       rstd.data_ptr<float>(), gamma.data_ptr(), dx.data_ptr(),
+                                       part_g.data_ptr<float>(), rms ? nullptr : part_b.data_ptr<float>(), rows,
+                                       static_cast<int>(H), rms, dtype_code(x), dtype_code(gamma), cur_stream());
+    damd_norm_wgrad_finalize_launch(part_g.data_ptr<float>(), rms ? nullptr : part_b.data_ptr<float>(), W,
+                                    static_cast<int>(H), dgamma.data_ptr(), rms ? nullptr : dbeta.data_ptr(),
+                                    dtype_code(gamma), cur_stream());
+  } else {
+    dgamma.zero_();
+    dbeta.zero_();
   }
   return {dx, dgamma, dbeta};
 }

@@ -117,30 +117,36 @@ lm_ce_bwd_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ 
 }
 
 // ---- bias gradient: out[n] = sum_m g[m, n] -----------------------------------------------
-constexpr int kBGCols = 512;  // columns per workgroup (64 lanes x 8)
+// Workgroup = 16 column lanes (8 columns each, one 16-byte load) x 16 row lanes; each
+// workgroup sums a [rows_per_split, 128] slab; the finalize pass adds <= 32 partials/column.
+constexpr int kBGCols = 128;
+constexpr int kBGRowLanes = 16;
 
 __global__ void __launch_bounds__(256)
 bias_grad_partial_kernel(const bf16_t* __restrict__ g, int64_t M, int N, int64_t rows_per_split,
                          float* __restrict__ part) {
-  const int lane = threadIdx.x & 63, wr = threadIdx.x >> 6;
-  const int col = blockIdx.x * kBGCols + lane * 8;
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * kBGCols + cl * 8;
   const int64_t r0 = blockIdx.y * rows_per_split;
   const int64_t r1 = min(M, r0 + rows_per_split);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (col < N) {
-    for (int64_t r = r0 + wr; r < r1; r += 4) {
+    for (int64_t r = r0 + rl; r < r1; r += kBGRowLanes) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + r * N + col);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(v.v[j]);
     }
   }
-  __shared__ float red[4][kBGCols];
+  __shared__ float red[kBGRowLanes][kBGCols + 4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[wr][lane * 8 + j] = acc[j];
+  for (int j = 0; j < 8; ++j) red[rl][cl * 8 + j] = acc[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < kBGCols; c += 256) {
-    const int gc = blockIdx.x * kBGCols + c;
-    if (gc < N) part[static_cast<int64_t>(blockIdx.y) * N + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (threadIdx.x < kBGCols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kBGRowLanes; ++k) s += red[k][threadIdx.x];
+    const int gc = blockIdx.x * kBGCols + threadIdx.x;
+    if (gc < N) part[static_cast<int64_t>(blockIdx.y) * N + gc] = s;
   }
 }
 
@@ -181,8 +187,9 @@ void damd_lm_ce_bwd_launch(const void* logits, const int64_t* labels, const floa
 
 int damd_bias_grad_splits(int64_t M, int N) {
   const int col_blocks = (N + kBGCols - 1) / kBGCols;
-  int splits = static_cast<int>((2048 + col_blocks - 1) / col_blocks);  // ~2048 workgroups
-  const int64_t max_splits = (M + 63) / 64;                             // >= 64 rows per split
+  int splits = static_cast<int>((1024 + col_blocks - 1) / col_blocks);  // ~1024 workgroups
+  if (splits > 32) splits = 32;                                         // finalize adds <= 32
+  const int64_t max_splits = (M + 127) / 128;                           // >= 128 rows per split
   if (splits > max_splits) splits = static_cast<int>(max_splits);
   return splits < 1 ? 1 : splits;
 }

@@ -190,13 +190,32 @@ norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* 
       }
     }
   }
+  // block-level reduction of the 4 waves' column partials -> one partial row per block
+  constexpr int kW = kNormThreads / kWave;
+  __shared__ __attribute__((aligned(16))) float red[kW][NV * kWave * kVecElems];
+  const int w = threadIdx.x / kWave;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c = (j * kWave + lane) * kVecElems;
-    if (c < H) {
-      Vec8<float>::st(part_g + wave_id * H + c, ag[j]);
-      if (!RMS) Vec8<float>::st(part_b + wave_id * H + c, ab[j]);
+  for (int pass = 0; pass < (RMS ? 1 : 2); ++pass) {
+    float* out = pass == 0 ? part_g : part_b;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * kWave + lane) * kVecElems;
+      Vec8<float>::st(&red[w][c], pass == 0 ? ag[j] : ab[j]);
     }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int c = (j * kWave + lane) * kVecElems;
+        if (c < H) {
+          float s[kVecElems];
+#pragma unroll
+          for (int k = 0; k < kVecElems; ++k) s[k] = red[0][c + k] + red[1][c + k] + red[2][c + k] + red[3][c + k];
+          Vec8<float>::st(out + static_cast<int64_t>(blockIdx.x) * H + c, s);
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -256,6 +275,44 @@ col_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int W
   }
 }
 
+// dgamma / dbeta from [W, H] fp32 partial rows, written directly in the weight dtype (no
+// atomics, no pre-zeroed output, no cast kernel).  grid = (ceil(H/128), 2: gamma | beta),
+// 256 threads = 32 column lanes (4 columns, one 16-byte load) x 8 row lanes.
+template <typename WT>
+__global__ void __launch_bounds__(256)
+wgrad_finalize_kernel(const float* __restrict__ part_g, const float* __restrict__ part_b, int W, int H,
+                      WT* __restrict__ dg, WT* __restrict__ db) {
+  const float* part = blockIdx.y == 0 ? part_g : part_b;
+  WT* out = blockIdx.y == 0 ? dg : db;
+  if (part == nullptr) return;  // RMSNorm: no beta (uniform per block)
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int col = blockIdx.x * 128 + cl * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((H & 3) == 0) {
+    if (col < H)
+      for (int w = rl; w < W; w += 8) {
+        const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(w) * H + col);
+        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+      }
+  } else {
+    for (int w = rl; w < W; w += 8)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (col + k < H) acc[k] += part[static_cast<int64_t>(w) * H + col + k];
+  }
+  __shared__ float red[8][128];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[rl][cl * 4 + k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int c = blockIdx.x * 128 + threadIdx.x;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][threadIdx.x];
+    if (c < H) Elem<WT>::st(out, c, s);
+  }
+}
+
 }  // namespace damd
 
 using namespace damd;
@@ -289,10 +346,12 @@ void fwd_dispatch(const void* x, const void* g, const void* b, void* y, float* m
   DAMD_CHECK_LAUNCH();
 }
 
+// returns the number of partial rows written (one per block on the register-resident path,
+// one per wave on the generic path)
 template <typename T, typename WT, bool RMS>
-void bwd_dispatch(const void* dy, const void* x, const float* mean, const float* rstd, const void* g,
-                  void* dx, float* part_g, float* part_b, int64_t rows, int H, int n_blocks,
-                  hipStream_t st) {
+int bwd_dispatch(const void* dy, const void* x, const float* mean, const float* rstd, const void* g,
+                 void* dx, float* part_g, float* part_b, int64_t rows, int H, int n_blocks,
+                 hipStream_t st) {
   const dim3 grid(n_blocks), block(kNormThreads);
   const T* dyp = static_cast<const T*>(dy);
   const T* xp = static_cast<const T*>(x);
@@ -301,6 +360,7 @@ void bwd_dispatch(const void* dy, const void* x, const float* mean, const float*
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
   const bool vec_ok = (H % kVecElems) == 0 && nv <= 4;  // 5*NV*8 live fp32 regs
 #define BWD_NV(N) hipLaunchKernelGGL((norm_bwd_kernel<T, WT, N, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H)
+  int W = n_blocks;
   if (vec_ok) {
     switch (nv) {
       case 1: BWD_NV(1); break;
@@ -309,9 +369,11 @@ void bwd_dispatch(const void* dy, const void* x, const float* mean, const float*
     }
   } else {
     hipLaunchKernelGGL((norm_bwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H);
+    W = n_blocks * (kNormThreads / kWave);
   }
 #undef BWD_NV
   DAMD_CHECK_LAUNCH();
+  return W;
 }
 }  // namespace
 
@@ -336,17 +398,31 @@ int damd_norm_bwd_blocks(int64_t rows) {
   return static_cast<int>(b);
 }
 
-void damd_norm_bwd_launch(const void* dy, const void* x, const float* mean, const float* rstd,
-                          const void* gamma, void* dx, float* part_g, float* part_b, int64_t rows,
-                          int H, int rms, int x_dtype, int w_dtype, hipStream_t st) {
+int damd_norm_bwd_launch(const void* dy, const void* x, const float* mean, const float* rstd,
+                         const void* gamma, void* dx, float* part_g, float* part_b, int64_t rows,
+                         int H, int rms, int x_dtype, int w_dtype, hipStream_t st) {
   const int nb = damd_norm_bwd_blocks(rows);
-#define BD(T, WT) do { if (rms) bwd_dispatch<T, WT, true>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); \
-                       else bwd_dispatch<T, WT, false>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); } while (0)
+  int W = 0;
+#define BD(T, WT) do { if (rms) W = bwd_dispatch<T, WT, true>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); \
+                       else W = bwd_dispatch<T, WT, false>(dy, x, mean, rstd, gamma, dx, part_g, part_b, rows, H, nb, st); } while (0)
   if (x_dtype == 1 && w_dtype == 1) BD(bf16_t, bf16_t);
   else if (x_dtype == 1) BD(bf16_t, float);
   else if (w_dtype == 1) BD(float, bf16_t);
   else BD(float, float);
 #undef BD
+  return W;
+}
+
+void damd_norm_wgrad_finalize_launch(const float* part_g, const float* part_b, int W, int H, void* dgamma,
+                                     void* dbeta, int w_dtype, hipStream_t st) {
+  const dim3 grid((H + 127) / 128, 2);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL((wgrad_finalize_kernel<bf16_t>), grid, dim3(256), 0, st, part_g, part_b, W, H,
+                       static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta));
+  else
+    hipLaunchKernelGGL((wgrad_finalize_kernel<float>), grid, dim3(256), 0, st, part_g, part_b, W, H,
+                       static_cast<float*>(dgamma), static_cast<float*>(dbeta));
+  DAMD_CHECK_LAUNCH();
 }
 
 void damd_col_reduce_launch(const float* part, float* out, int W, int H, hipStream_t st) {

@@ -11,3 +11,7 @@ timeout -k 10 300 python -m determined_amd.benchmarks.gpt2 --mb 8 --steps 10 --w
 tail -1 gpurun_out/gpt2_bench.log
 timeout -k 10 300 python -m determined_amd.benchmarks.gpt2 --mb 16 --steps 10 --warmup 3 > gpurun_out/gpt2_bench16.log 2>&1 || { echo gpt2 bench16 failed; tail -30 gpurun_out/gpt2_bench16.log; exit 1; }
 tail -1 gpurun_out/gpt2_bench16.log
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof_gpt2
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gpt2 -o run --output-format csv -- python -m determined_amd.benchmarks.gpt2 --mb 8 --steps 5 --warmup 3 > gpurun_out/prof_gpt2.log 2>&1
+echo "rocprof exit $?"

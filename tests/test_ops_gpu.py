@@ -65,7 +65,9 @@ def test_fused_adamw_master_weights_bf16(ops):
     for a, b in zip(ours, ref):
         st = o_ours.state[a]
         torch.testing.assert_close(st["master"], b.detach(), rtol=1e-5, atol=1e-6)
-        torch.testing.assert_close(a.detach().float(), b.detach().to(torch.bfloat16).float(), rtol=0, atol=0)
+        # the bf16 param is exactly the RNE rounding of its own fp32 master (which matches the
+        # reference to 1e-5; comparing against the reference's rounding flips 1 ulp at ties)
+        torch.testing.assert_close(a.detach().float(), st["master"].to(torch.bfloat16).float(), rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("nesterov,dampening", [(False, 0.0), (True, 0.0), (False, 0.1)])
