@@ -5,6 +5,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <vector>
 
 namespace damd {
@@ -251,7 +252,8 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, cons
   const int64_t rows = x.numel() / H;
   auto dx = at::empty_like(x);
   auto fopts = x.options().dtype(at::kFloat);
-  // weight gradients come out in the weight dtype: per-block partials + one finalize pass
+  // weight gradients come out in the weight dtype, finalized inside the backward kernel
+  // (register-resident path) or by one finalize pass over per-wave partials (generic path)
   auto dgamma = at::empty({H}, gamma.options());
   auto dbeta = rms ? at::empty({0}, gamma.options()) : at::empty({H}, gamma.options());
   if (rows > 0) {
@@ -493,8 +495,10 @@ at::Tensor bias_grad(const at::Tensor& g, at::ScalarType out_dtype) {
   auto out = at::empty({N}, g.options().dtype(out_dtype));
   const int splits = damd_bias_grad_splits(M, static_cast<int>(N));
   auto part = at::empty({splits, N}, g.options().dtype(at::kFloat));
-  damd_bias_grad_launch(g.data_ptr(), M, static_cast<int>(N), splits, part.data_ptr<float>(), out.data_ptr(),
-                        out_dtype == at::kFloat ? 0 : 1, cur_stream());
+  damd_bias_grad_launch(g.data_ptr(), M, static_cast<int>(N), splits, part.data_ptr<float>(), nullptr, 0,
+                        cur_stream());  // partial rows only
+  damd_norm_wgrad_finalize_launch(part.data_ptr<float>(), nullptr, splits, static_cast<int>(N), out.data_ptr(),
+                                  nullptr, out_dtype == at::kFloat ? 0 : 1, cur_stream());
   return out;
 }
 

@@ -11,7 +11,7 @@
 //   Replaces: slice + reshape + bf16->fp32 copy + softmax fwd + softmax bwd + fills.
 //
 // bias_grad: column sums of a [M, N] bf16 gradient (the bias gradient of a Linear) with
-//   16-byte loads, row-split partials in fp32 and a second tiny pass.
+//   16-byte loads into row-split fp32 partials; the wide finalize of norm.hip finishes them.
 
 #include "common.h"
 
@@ -150,16 +150,6 @@ bias_grad_partial_kernel(const bf16_t* __restrict__ g, int64_t M, int N, int64_t
   }
 }
 
-template <typename OT>
-__global__ void __launch_bounds__(256)
-bias_grad_finalize_kernel(const float* __restrict__ part, int splits, int N, OT* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[static_cast<int64_t>(k) * N + c];
-  Elem<OT>::st(out, c, s);
-}
-
 }  // namespace fused
 }  // namespace damd
 
@@ -194,20 +184,14 @@ int damd_bias_grad_splits(int64_t M, int N) {
   return splits < 1 ? 1 : splits;
 }
 
-void damd_bias_grad_launch(const void* g, int64_t M, int N, int splits, float* part, void* out, int out_dtype,
-                           hipStream_t st) {
+// Partial column sums [splits, N] (fp32); the host finishes with the wide column-sum pass
+// of norm.hip (damd_norm_wgrad_finalize_launch), which writes the output dtype directly.
+void damd_bias_grad_launch(const void* g, int64_t M, int N, int splits, float* part, void* /*out*/,
+                           int /*out_dtype*/, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   const int64_t rps = (M + splits - 1) / splits;
   dim3 grid((N + kBGCols - 1) / kBGCols, splits);
   hipLaunchKernelGGL(bias_grad_partial_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g), M, N, rps, part);
-  DAMD_CHECK_LAUNCH();
-  const dim3 g2((N + 255) / 256);
-  if (out_dtype == 0)
-    hipLaunchKernelGGL((bias_grad_finalize_kernel<float>), g2, dim3(256), 0, st, part, splits, N,
-                       static_cast<float*>(out));
-  else
-    hipLaunchKernelGGL((bias_grad_finalize_kernel<bf16_t>), g2, dim3(256), 0, st, part, splits, N,
-                       static_cast<bf16_t*>(out));
   DAMD_CHECK_LAUNCH();
 }
 

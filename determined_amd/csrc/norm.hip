@@ -132,7 +132,9 @@ norm_fwd_generic_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, c
 }
 
 // ------------------------------------------------------------------ backward (register-resident)
-// part_g / part_b: [n_waves_total, H] fp32 partials for dgamma / dbeta.
+// Weight gradients: the 4 waves' column partials are reduced in LDS and each block writes one
+// fp32 partial row (part_g / part_b: [gridDim.x, H]); wgrad_finalize_kernel sums the rows and
+// writes dgamma / dbeta in the weight dtype.
 template <typename T, typename WT, int NV, bool RMS>
 __global__ void __launch_bounds__(kNormThreads)
 norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean_in,
@@ -191,6 +193,8 @@ norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* 
     }
   }
   // block-level reduction of the 4 waves' column partials -> one partial row per block
+  // (float atomics into one row from every block run ~14x below the atomic rate on MI355X,
+  // so the cross-block sum is a separate wide finalize pass instead)
   constexpr int kW = kNormThreads / kWave;
   __shared__ __attribute__((aligned(16))) float red[kW][NV * kWave * kVecElems];
   const int w = threadIdx.x / kWave;
@@ -275,41 +279,32 @@ col_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int W
   }
 }
 
-// dgamma / dbeta from [W, H] fp32 partial rows, written directly in the weight dtype (no
-// atomics, no pre-zeroed output, no cast kernel).  grid = (ceil(H/128), 2: gamma | beta),
-// 256 threads = 32 column lanes (4 columns, one 16-byte load) x 8 row lanes.
+// Column sums of [W, H] fp32 partial rows written directly in the output dtype (no atomics,
+// no pre-zeroed output, no cast kernel).  Latency-bound, so it is made WIDE: grid =
+// (ceil(H/32), 2: gamma | beta), 256 threads = 32 column lanes x 8 row lanes (one 128-byte
+// coalesced segment per row per wave).  Also used for Linear bias gradients (part_b = null).
 template <typename WT>
 __global__ void __launch_bounds__(256)
 wgrad_finalize_kernel(const float* __restrict__ part_g, const float* __restrict__ part_b, int W, int H,
                       WT* __restrict__ dg, WT* __restrict__ db) {
   const float* part = blockIdx.y == 0 ? part_g : part_b;
   WT* out = blockIdx.y == 0 ? dg : db;
-  if (part == nullptr) return;  // RMSNorm: no beta (uniform per block)
+  if (part == nullptr) return;  // no second output (uniform per block)
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
-  const int col = blockIdx.x * 128 + cl * 4;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if ((H & 3) == 0) {
-    if (col < H)
-      for (int w = rl; w < W; w += 8) {
-        const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(w) * H + col);
-        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
-      }
-  } else {
-    for (int w = rl; w < W; w += 8)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (col + k < H) acc[k] += part[static_cast<int64_t>(w) * H + col + k];
+  const int col = blockIdx.x * 32 + cl;
+  float acc = 0.f;
+  if (col < H) {
+#pragma unroll 4
+    for (int w = rl; w < W; w += 8) acc += part[static_cast<int64_t>(w) * H + col];
   }
-  __shared__ float red[8][128];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[rl][cl * 4 + k] = acc[k];
+  __shared__ float red[8][33];
+  red[rl][cl] = acc;
   __syncthreads();
-  if (threadIdx.x < 128) {
-    const int c = blockIdx.x * 128 + threadIdx.x;
+  if (threadIdx.x < 32) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += red[k][threadIdx.x];
-    if (c < H) Elem<WT>::st(out, c, s);
+    if (col < H) Elem<WT>::st(out, col, s);
   }
 }
 
@@ -398,6 +393,8 @@ int damd_norm_bwd_blocks(int64_t rows) {
   return static_cast<int>(b);
 }
 
+// Returns the number of partial rows written to part_g / part_b (input of
+// damd_norm_wgrad_finalize_launch).
 int damd_norm_bwd_launch(const void* dy, const void* x, const float* mean, const float* rstd,
                          const void* gamma, void* dx, float* part_g, float* part_b, int64_t rows,
                          int H, int rms, int x_dtype, int w_dtype, hipStream_t st) {
@@ -415,7 +412,7 @@ int damd_norm_bwd_launch(const void* dy, const void* x, const float* mean, const
 
 void damd_norm_wgrad_finalize_launch(const float* part_g, const float* part_b, int W, int H, void* dgamma,
                                      void* dbeta, int w_dtype, hipStream_t st) {
-  const dim3 grid((H + 127) / 128, 2);
+  const dim3 grid((H + 31) / 32, 2);
   if (w_dtype == 1)
     hipLaunchKernelGGL((wgrad_finalize_kernel<bf16_t>), grid, dim3(256), 0, st, part_g, part_b, W, H,
                        static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta));
