@@ -210,8 +210,9 @@ PYBIND11_MODULE(_native, m) {
       .def("set_agent_enabled", &Scheduler::set_agent_enabled)
       .def("add_request",
            [](Scheduler& s, const std::string& alloc_id, const std::string& job_id, int slots, int priority,
-              double weight, int64_t order, bool preemptible) {
+              double weight, int64_t order, bool preemptible, const std::vector<std::string>& excluded_agents) {
              Request r;
+             r.excluded_agents = excluded_agents;
              r.alloc_id = alloc_id;
              r.job_id = job_id;
              r.slots = slots;
@@ -222,7 +223,8 @@ PYBIND11_MODULE(_native, m) {
              s.add_request(r);
            },
            py::arg("alloc_id"), py::arg("job_id"), py::arg("slots"), py::arg("priority") = 42,
-           py::arg("weight") = 1.0, py::arg("order") = 0, py::arg("preemptible") = true)
+           py::arg("weight") = 1.0, py::arg("order") = 0, py::arg("preemptible") = true,
+           py::arg("excluded_agents") = std::vector<std::string>())
       .def("remove_request", &Scheduler::remove_request)
       .def("set_priority", &Scheduler::set_priority)
       .def("set_weight", &Scheduler::set_weight)

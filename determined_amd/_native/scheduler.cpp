@@ -95,9 +95,12 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
   // shared fit
   const AgentState* best = nullptr;
   double best_score = -1;
+  auto excluded = [&r](const std::string& id) {
+    return std::find(r.excluded_agents.begin(), r.excluded_agents.end(), id) != r.excluded_agents.end();
+  };
   for (const auto& kv : agents) {
     const AgentState& a = kv.second;
-    if (!a.enabled) continue;
+    if (!a.enabled || excluded(a.id)) continue;
     if (r.slots > a.empty()) continue;
     const double s = score(r, a);
     if (s > best_score || (s == best_score && best && a.id < best->id)) {
@@ -116,7 +119,7 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
   std::map<int, std::vector<const AgentState*>, std::greater<int>> by_slots;
   for (const auto& kv : agents) {
     const AgentState& a = kv.second;
-    if (!a.enabled || a.used() != 0 || a.num_slots == 0) continue;
+    if (!a.enabled || a.used() != 0 || a.num_slots == 0 || excluded(a.id)) continue;
     by_slots[a.num_slots].push_back(&a);
   }
   for (auto& g : by_slots) {

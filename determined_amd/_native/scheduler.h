@@ -10,6 +10,7 @@
 
 #include <cstdint>
 #include <map>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,7 @@ struct Request {
   bool preemptible = true;
   bool allocated = false;
   bool preempting = false;  // release already requested
+  std::vector<std::string> excluded_agents;  // log-policy exclude_node blocklist
   // agent id -> slot indices
   std::vector<std::pair<std::string, std::vector<int>>> assignment;
 };

@@ -65,6 +65,8 @@ class TrialRec:
         self.total_batches = 0
         self.early_exit: Optional[str] = None
         self.warm_start: Optional[str] = None
+        self.no_retry = False                  # log policy cancel_retries matched
+        self.excluded_agents: List[str] = []  # log policy exclude_node matched
 
     def searcher_state(self) -> Dict[str, Any]:
         return {"ops": self.ops, "close_requested": self.close_requested, "early_exit": self.early_exit}
@@ -117,12 +119,19 @@ class Master:
             self.cv.notify_all()
 
     def _tick_loop(self) -> None:
+        last_cleanup = 0.0
         while True:
             with self.lock:
                 if self._closed:
                     return
                 self._check_agents()
                 self._schedule()
+                if time.time() - last_cleanup > 600:
+                    last_cleanup = time.time()
+                    try:
+                        self.cleanup_logs()
+                    except Exception as e:  # retention is best effort
+                        logger.warning(f"log retention cleanup failed: {e}")
                 self.cv.wait(1.0)
 
     def _restore(self) -> None:
@@ -440,7 +449,8 @@ class Master:
         self.allocations[aid] = a
         prio = exp.config["resources"].get("priority")
         self.sched.add_request(aid, f"exp-{exp.id}", slots, int(prio) if prio is not None else 42,
-                               float(exp.config["resources"].get("weight", 1)), self._next_order(), True)
+                               float(exp.config["resources"].get("weight", 1)), self._next_order(), True,
+                               list(tr.excluded_agents))
         self.cv.notify_all()
 
     def create_command(self, cmd: List[str], slots: int = 0, env: Optional[Dict[str, str]] = None,
@@ -640,7 +650,7 @@ class Master:
             tr.restarts += 1
             max_restarts = int(exp.config.get("max_restarts", 5))
             logger.warning(f"trial {tr.id} failed (exit {a.exit_codes}); restart {tr.restarts}/{max_restarts}")
-            if tr.restarts > max_restarts:
+            if tr.restarts > max_restarts or tr.no_retry:
                 ops = self._finish_trial(exp, tr, "ERROR")
             elif exp.state == "ACTIVE":
                 self._request_allocation(exp, tr)
@@ -771,7 +781,61 @@ class Master:
             self.db.conn.executemany(
                 "INSERT INTO task_logs (task_id, allocation_id, rank, ts, log) VALUES (?,?,?,?,?)",
                 [(task_id, allocation_id, l.get("rank"), now, l["log"]) for l in logs])
+            self._apply_log_policies(task_id, allocation_id, logs)
             self.cv.notify_all()
+
+    def _apply_log_policies(self, task_id: str, allocation_id: Optional[str], logs: List[Dict[str, Any]]) -> None:
+        """Experiment ``log_policies`` (reference ``master/internal/logpattern``): a regex match in a
+        trial's logs can cancel its remaining restarts (``cancel_retries``) or keep its next
+        allocations off the agent that produced the line (``exclude_node``)."""
+        if not task_id.startswith("trial-"):
+            return
+        try:
+            exp, tr = self._trial(int(task_id.split("-", 1)[1]))
+        except (KeyError, ValueError):
+            return
+        policies = exp.config.get("log_policies") or []
+        if not policies:
+            return
+        import re
+
+        a = self.allocations.get(allocation_id) if allocation_id else tr.allocation
+        for pol in policies:
+            try:
+                rx = re.compile(pol["pattern"])
+            except (re.error, KeyError, TypeError):
+                continue
+            if not any(rx.search(l.get("log", "")) for l in logs):
+                continue
+            act = (pol.get("action") or {}).get("type")
+            if act == "cancel_retries" and not tr.no_retry:
+                tr.no_retry = True
+                logger.info(f"trial {tr.id}: log policy {pol['pattern']!r} matched; retries cancelled")
+            elif act == "exclude_node" and a is not None:
+                for agent_id, _ in a.assignment:
+                    if agent_id not in tr.excluded_agents:
+                        tr.excluded_agents.append(agent_id)
+                        logger.info(f"trial {tr.id}: log policy {pol['pattern']!r} matched; excluding {agent_id}")
+
+    def cleanup_logs(self, now: Optional[float] = None) -> int:
+        """Log retention (``retention_policy.log_retention_days``, experiment config or master
+        default ``DET_LOG_RETENTION_DAYS``): delete logs of trials that ended longer ago."""
+        now = time.time() if now is None else now
+        deleted = 0
+        default_days = os.environ.get("DET_LOG_RETENTION_DAYS")
+        with self.lock:
+            for row in self.db.all("SELECT id, config FROM experiments"):
+                days = ((row["config"] or {}).get("retention_policy") or {}).get("log_retention_days")
+                if days is None and default_days is not None:
+                    days = int(default_days)
+                if days is None or int(days) < 0:
+                    continue
+                cutoff = now - int(days) * 86400
+                for t in self.db.all("SELECT id FROM trials WHERE experiment_id=? AND end_time IS NOT NULL AND "
+                                     "end_time < ?", [row["id"], cutoff]):
+                    cur = self.db.execute("DELETE FROM task_logs WHERE task_id=?", [f"trial-{t['id']}"])
+                    deleted += cur.rowcount or 0
+        return deleted
 
     def get_logs(self, task_id: str, after_id: int = 0, limit: int = 10000) -> List[Dict[str, Any]]:
         return self.db.all("SELECT id, rank, ts, log FROM task_logs WHERE task_id=? AND id>? ORDER BY id LIMIT ?",

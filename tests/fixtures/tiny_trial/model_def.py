@@ -53,3 +53,13 @@ class TinyTrial(pytorch.PyTorchTrial):
 
     def build_validation_data_loader(self):
         return pytorch.DataLoader(_DS(64, 1), batch_size=16)
+
+
+class NoisyFailTrial(TinyTrial):
+    """Prints a recognisable error line and fails every attempt (log-policy tests)."""
+
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        if batch_idx >= 1:
+            print("FATAL: ECC error detected on device", flush=True)
+            raise RuntimeError("hardware fault (simulated)")
+        return super().train_batch(batch, epoch_idx, batch_idx)

@@ -272,3 +272,35 @@ def test_custom_searcher_local_runner(cluster):
     assert e["state"] == "COMPLETED" and method.created == 2
     ts = _trials(cluster, eid)
     assert sorted(t["total_batches"] for t in ts) == [8, 8]
+
+
+def test_log_policy_cancel_retries_and_retention(cluster):
+    eid = _create(cluster, {"name": "logpolicy", "max_restarts": 5, "hyperparameters": HP,
+                            "entrypoint": "model_def:NoisyFailTrial",
+                            "log_policies": [{"pattern": "ECC error", "action": {"type": "cancel_retries"}},
+                                             {"pattern": "ECC error", "action": {"type": "exclude_node"}}],
+                            "retention_policy": {"log_retention_days": 0},
+                            "searcher": {"name": "single", "metric": "validation_loss",
+                                         "max_length": {"batches": 6}}})
+    e = _wait(cluster, eid)
+    (t,) = _trials(cluster, eid)
+    assert e["state"] == "ERROR" and t["state"] == "ERROR" and t["restarts"] == 1  # no further retries
+    m = cluster["master"].master
+    (tr,) = m.experiments[eid].trials.values()
+    assert tr.no_retry and tr.excluded_agents == ["e2e-agent"]
+    assert m.cleanup_logs(now=time.time() + 10) > 0
+
+
+def test_scheduler_excluded_agents():
+    from determined_amd._native import load
+
+    n = load()
+    s = n.Scheduler(n.Policy.PRIORITY, n.Fit.BEST, True)
+    s.add_agent("a", 2)
+    s.add_agent("b", 2)
+    s.add_request("r1", "j1", 2, excluded_agents=["a"])
+    d = s.schedule()
+    assert d["allocated"] == ["r1"]
+    assert [ag for ag, _ in s.requests()["r1"]["assignment"]] == ["b"]
+    s.add_request("r2", "j2", 2, excluded_agents=["a"])
+    assert s.schedule()["allocated"] == []  # only "a" is free and it is excluded
