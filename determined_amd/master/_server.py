@@ -285,6 +285,10 @@ def build_routes(m: Master) -> List[Route]:
             raise HTTPError(404, f"checkpoint {u} not found")
         if "metadata" in b:
             m.db.update("checkpoints", "uuid", u, metadata=b["metadata"])
+        if "resources" in b:  # partial GC (exec/gc_checkpoints.py --globs) reports what is left
+            m.db.update("checkpoints", "uuid", u, resources=b["resources"])
+        if b.get("state") in ("PARTIALLY_DELETED", "DELETED"):
+            m.db.update("checkpoints", "uuid", u, state=b["state"])
         return {}
 
     @route("DELETE", r"/api/v1/checkpoints/([0-9a-f\-]+)")
