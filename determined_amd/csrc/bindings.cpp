@@ -53,12 +53,12 @@ void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
-                        float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t);
+                        float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*);
 void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
                                hipStream_t);
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
                         const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
-                        hipStream_t);
+                        hipStream_t, const uint8_t*);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
                                      int, int, float, int, hipStream_t);
@@ -301,7 +301,7 @@ bool bn_supported(const at::Tensor& x) {
 std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                                    const c10::optional<at::Tensor>& running_mean,
                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps,
-                                   const c10::optional<at::Tensor>& residual, bool relu) {
+                                   const c10::optional<at::Tensor>& residual, bool relu, bool want_mask) {
   TORCH_CHECK(bn_supported(x), "bn_act_fwd: unsupported input layout/shape");
   const int64_t C = bn_channels(x);
   const int64_t M = x.numel() / C;
@@ -325,11 +325,16 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
   auto part = at::empty({nb, 2, C}, fopts);
   auto stats = at::empty({4, C}, fopts);  // mean, invstd, scale, shift
   auto y = at::empty_like(x);
+  // ReLU bit mask (1 byte per 8 channels) for the residual+ReLU case: the backward reads it
+  // instead of the residual tensor
+  const bool mk = want_mask && relu && rp != nullptr;
+  at::Tensor mask = mk ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : at::empty({0}, x.options().dtype(at::kByte));
   damd_bn_fwd_launch(x.data_ptr(), rp, y.data_ptr(), M, static_cast<int>(C), weight.data_ptr(), bias.data_ptr(), rm, rv,
                      static_cast<float>(momentum), static_cast<float>(eps), part.data_ptr<float>(),
                      stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
-                     stats[3].data_ptr<float>(), relu, dtype_code(x), dtype_code(weight), cur_stream());
-  return {y, stats};
+                     stats[3].data_ptr<float>(), relu, dtype_code(x), dtype_code(weight), cur_stream(),
+                     mk ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, stats, mask};
 }
 
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
@@ -351,7 +356,8 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
 
 std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
                                    const c10::optional<at::Tensor>& residual, const at::Tensor& stats,
-                                   const at::Tensor& weight, bool relu, bool need_dres) {
+                                   const at::Tensor& weight, bool relu, bool need_dres,
+                                   const c10::optional<at::Tensor>& mask) {
   check_bn_tensor(dy, x, "dy");
   const int64_t C = bn_channels(x);
   const int64_t M = x.numel() / C;
@@ -359,6 +365,12 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   if (residual.has_value() && residual->defined()) {
     check_bn_tensor(*residual, x, "residual");
     rp = residual->data_ptr();
+  }
+  const uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined() && mask->numel() > 0) {
+    TORCH_CHECK(relu && mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() == M * C / 8 &&
+                mask->device() == x.device(), "bn_act_bwd: mask must be a uint8 [M*C/8] tensor (ReLU path)");
+    mp = mask->data_ptr<uint8_t>();
   }
   auto fopts = x.options().dtype(at::kFloat);
   const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
@@ -374,7 +386,7 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
                      stats[1].data_ptr<float>(), stats[2].data_ptr<float>(), stats[3].data_ptr<float>(),
                      part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(),
                      dx.data_ptr(), write_dres ? dres.data_ptr() : nullptr, relu, dtype_code(x), dtype_code(weight),
-                     cur_stream());
+                     cur_stream(), mp);
   return {dx, dgamma, dbeta, dres};
 }
 

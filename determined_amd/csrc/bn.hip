@@ -198,10 +198,13 @@ bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, int
 }
 
 // ----------------------------------------------------------------------------- fwd apply
-template <typename T, bool RES, bool RELU>
+// WMASK (residual + ReLU training path): also write one byte per 8-channel vector whose bit k is
+// [output k > 0].  The backward then reads M*C/8 bytes instead of the residual tensor
+// (M*C*2 bytes) in both of its passes to rebuild the ReLU mask.
+template <typename T, bool RES, bool RELU, bool WMASK = false>
 __global__ void __launch_bounds__(kBNThreads)
 bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
-                const T* __restrict__ res, T* __restrict__ y, int64_t V, int TPR) {
+                const T* __restrict__ res, T* __restrict__ y, int64_t V, int TPR, uint8_t* __restrict__ mask = nullptr) {
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;  // multiple of TPR
   const int cg = static_cast<int>(T0 % TPR);
@@ -220,17 +223,25 @@ bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ scale, const 
       a[k] = o;
     }
     V8<T>::st(y + v * 8, a);
+    if (WMASK) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bits |= (a[k] > 0.f ? 1u : 0u) << k;
+      mask[v] = static_cast<uint8_t>(bits);
+    }
   }
 }
 
 // ----------------------------------------------------------------------------- bwd reduce
 // part: [nb][2][C] = (sum dy', sum dy' * (x - mean))
-template <typename T, bool RES, bool RELU>
+// MASKED: the ReLU mask comes from the forward's bit mask instead of recomputing it from
+// x (and the residual), see bn_apply_kernel<..., WMASK>.
+template <typename T, bool RES, bool RELU, bool MASKED = false>
 __global__ void __launch_bounds__(kBNThreads)
 bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
                      const float* __restrict__ mean, const float* __restrict__ scale,
                      const float* __restrict__ shift, int64_t M, int C, int64_t rows_per_block,
-                     float* __restrict__ part) {
+                     float* __restrict__ part, const uint8_t* __restrict__ mask = nullptr) {
   const Geo g = geo(C);
   const int tid = threadIdx.x;
   const int cg0 = g.TPR <= kBNThreads ? tid % g.TPR : tid;
@@ -248,19 +259,23 @@ bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T*
     int64_t r = r0 + rsub;
     for (; r + g.RS < r1; r += 2 * g.RS) {
       float d[2][8], a[2][8], rr[2][8];
+      uint32_t mb[2] = {0u, 0u};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int64_t off = (r + u * g.RS) * C + cg * 8;
         V8<T>::ld(dy + off, d[u]);
         V8<T>::ld(x + off, a[u]);
-        if (RES && RELU) V8<T>::ld(res + off, rr[u]);
+        if (MASKED) mb[u] = mask[off >> 3];
+        else if (RES && RELU) V8<T>::ld(res + off, rr[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float dv = d[u][k];
-          if (RELU) {
+          if (MASKED) {
+            dv = (mb[u] >> k) & 1u ? dv : 0.f;
+          } else if (RELU) {
             float z = a[u][k] * sc[k] + sh[k];
             if (RES) z += rr[u][k];
             dv = z > 0.f ? dv : 0.f;
@@ -271,14 +286,18 @@ bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T*
     }
     for (; r < r1; r += g.RS) {
       float d[8], a[8], rr[8];
+      uint32_t mb = 0u;
       const int64_t off = r * C + cg * 8;
       V8<T>::ld(dy + off, d);
       V8<T>::ld(x + off, a);
-      if (RES && RELU) V8<T>::ld(res + off, rr);
+      if (MASKED) mb = mask[off >> 3];
+      else if (RES && RELU) V8<T>::ld(res + off, rr);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float dv = d[k];
-        if (RELU) {
+        if (MASKED) {
+          dv = (mb >> k) & 1u ? dv : 0.f;
+        } else if (RELU) {
           float z = a[k] * sc[k] + sh[k];
           if (RES) z += rr[k];
           dv = z > 0.f ? dv : 0.f;
@@ -334,12 +353,12 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
   }
 }
 
-template <typename T, bool RES, bool RELU, bool WRITE_DRES>
+template <typename T, bool RES, bool RELU, bool WRITE_DRES, bool MASKED = false>
 __global__ void __launch_bounds__(kBNThreads)
 bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
                     const float* __restrict__ scale, const float* __restrict__ shift,
                     const float* __restrict__ coef, int C, T* __restrict__ dx, T* __restrict__ dres, int64_t V,
-                    int TPR) {
+                    int TPR, const uint8_t* __restrict__ mask = nullptr) {
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
   const int cg = static_cast<int>(T0 % TPR);
@@ -350,13 +369,17 @@ bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* 
   if (RELU) { V8<float>::ld(scale + cg * 8, sc); V8<float>::ld(shift + cg * 8, sh); }
   for (int64_t v = T0; v < V; v += stride) {
     float d[8], a[8], rr[8], o[8];
+    uint32_t mb = 0u;
     V8<T>::ld(dy + v * 8, d);
     V8<T>::ld(x + v * 8, a);
-    if (RES && RELU) V8<T>::ld(res + v * 8, rr);
+    if (MASKED) mb = mask[v];
+    else if (RES && RELU) V8<T>::ld(res + v * 8, rr);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float dv = d[k];
-      if (RELU) {
+      if (MASKED) {
+        dv = (mb >> k) & 1u ? dv : 0.f;
+      } else if (RELU) {
         float z = a[k] * sc[k] + sh[k];
         if (RES) z += rr[k];
         dv = z > 0.f ? dv : 0.f;
@@ -405,7 +428,7 @@ int damd_bn_num_blocks(int64_t M, int C) {
 void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int C, const void* w, const void* b,
                         float* run_mean, float* run_var, float momentum, float eps, float* part, float* mean,
                         float* invstd, float* scale, float* shift, int relu, int x_dtype, int w_dtype,
-                        hipStream_t st) {
+                        hipStream_t st, uint8_t* mask) {
   int nb;
   const int64_t rpb = rows_per_block_for(M, C, &nb);
   if (x_dtype == 1)
@@ -422,8 +445,13 @@ void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int 
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
-#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR)
-  if (x_dtype == 1) {
+#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR, nullptr)
+  if (mask != nullptr && res && relu) {
+    if (x_dtype == 1)
+      hipLaunchKernelGGL((bn_apply_kernel<bf16_t, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift, static_cast<const bf16_t*>(res), static_cast<bf16_t*>(y), V, TPR, mask);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<float, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift, static_cast<const float*>(res), static_cast<float*>(y), V, TPR, mask);
+  } else if (x_dtype == 1) {
     if (res) { if (relu) APPLY(bf16_t, true, true); else APPLY(bf16_t, true, false); }
     else { if (relu) APPLY(bf16_t, false, true); else APPLY(bf16_t, false, false); }
   } else {
@@ -454,12 +482,18 @@ void damd_bn_apply_only_launch(const void* x, const void* res, void* y, int64_t 
 void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t M, int C, const float* mean,
                         const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                         void* dgamma, void* dbeta, void* dx, void* dres, int relu, int x_dtype, int w_dtype,
-                        hipStream_t st) {
+                        hipStream_t st, const uint8_t* mask) {
   int nb;
   const int64_t rpb = rows_per_block_for(M, C, &nb);
-  const bool has_res = res != nullptr;
-#define RED(T, R, A) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part)
-  if (x_dtype == 1) {
+  const bool has_res = res != nullptr || mask != nullptr;
+  const bool masked = mask != nullptr && relu;
+#define RED(T, R, A) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part, nullptr)
+  if (masked) {
+    if (x_dtype == 1)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, true, true, true>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, true, true, true>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dy), static_cast<const float*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask);
+  } else if (x_dtype == 1) {
     if (has_res) { if (relu) RED(bf16_t, true, true); else RED(bf16_t, true, false); }
     else { if (relu) RED(bf16_t, false, true); else RED(bf16_t, false, false); }
   } else {
@@ -477,8 +511,12 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
   const bool wd = dres != nullptr;
-#define BAP(T, R, A, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR)
-  if (x_dtype == 1) {
+#define BAP(T, R, A, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, nullptr)
+#define BAPM(T, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true, W, true>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, mask)
+  if (masked) {
+    if (x_dtype == 1) { if (wd) BAPM(bf16_t, true); else BAPM(bf16_t, false); }
+    else { if (wd) BAPM(float, true); else BAPM(float, false); }
+  } else if (x_dtype == 1) {
     if (has_res) { if (relu) { if (wd) BAP(bf16_t, true, true, true); else BAP(bf16_t, true, true, false); }
                    else { if (wd) BAP(bf16_t, true, false, true); else BAP(bf16_t, true, false, false); } }
     else { if (relu) { if (wd) BAP(bf16_t, false, true, true); else BAP(bf16_t, false, true, false); }
@@ -490,5 +528,6 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
            else { if (wd) BAP(float, false, false, true); else BAP(float, false, false, false); } }
   }
 #undef BAP
+#undef BAPM
   DAMD_CHECK_LAUNCH();
 }

@@ -3,7 +3,8 @@
 ``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and
 state-dict keys) whose forward takes an optional residual and applies ReLU in the same pass:
 ``y = relu(bn(x) + residual)``.  Training on a supported GPU tensor runs 2 kernels forward
-(stats, apply) and 2 backward (reduce, apply) instead of stock PyTorch's 7 HBM passes.
+(stats, apply) and 2 backward (reduce, apply) instead of stock PyTorch's 7 HBM passes; with a
+residual the forward also writes a ReLU bit mask so the backward never re-reads the residual.
 CPU tensors / unsupported shapes use the exact PyTorch composition.
 """
 
@@ -19,9 +20,12 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
         from determined_amd import ops
 
-        y, stats = ops.ext().bn_act_fwd(x, weight, bias, running_mean, running_var, float(momentum),
-                                        float(eps), residual, bool(relu))
-        ctx.save_for_backward(x, residual if residual is not None else None, stats, weight)
+        # residual + ReLU: the forward also emits a 1-bit-per-element ReLU mask, so the backward
+        # reads M*C/8 bytes instead of the residual tensor in both of its passes
+        y, stats, mask = ops.ext().bn_act_fwd(x, weight, bias, running_mean, running_var, float(momentum),
+                                              float(eps), residual, bool(relu), True)
+        masked = mask.numel() > 0
+        ctx.save_for_backward(x, None if masked else residual, stats, weight, mask if masked else None)
         ctx.relu = relu
         ctx.has_res = residual is not None
         return y
@@ -30,10 +34,11 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         from determined_amd import ops
 
-        x, residual, stats, weight = ctx.saved_tensors
+        x, residual, stats, weight, mask = ctx.saved_tensors
         mf = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy = dy.contiguous(memory_format=mf)
-        dx, dg, db, dres = ops.ext().bn_act_bwd(dy, x, residual, stats, weight, bool(ctx.relu), bool(ctx.has_res))
+        dx, dg, db, dres = ops.ext().bn_act_bwd(dy, x, residual, stats, weight, bool(ctx.relu), bool(ctx.has_res),
+                                                mask)
         return (dx, dg, db, None, None,
                 dres if ctx.has_res else None, None, None, None)
 
