@@ -126,6 +126,10 @@ class GPT2LMHeadModel(nn.Module):
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, mean=0.0, std=0.02)
 
+    def zero3_external_parameters(self):
+        """ZeRO-3: the tied LM head reads ``wte.weight`` in this module's forward."""
+        return [(self, self.wte.weight)]
+
     def num_parameters(self, exclude_embeddings: bool = False) -> int:
         n = sum(p.numel() for p in self.parameters())
         if exclude_embeddings:

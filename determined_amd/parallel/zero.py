@@ -1,4 +1,4 @@
-"""ZeRO data-parallel engine (stages 0/1/2) with a DeepSpeed-style API.
+"""ZeRO data-parallel engine (stages 0/1/2; stage 3 in ``zero3.py``) with a DeepSpeed-style API.
 
 The reference's ``DeepSpeedTrial`` drives a ``deepspeed.DeepSpeedEngine`` (reference
 ``harness/determined/pytorch/deepspeed/_deepspeed_trial.py:364`` ``_train_for_step`` calls
@@ -33,7 +33,7 @@ Memory layout (one flat buffer per parameter dtype):
 Gradient clipping uses the shard-local sum of squares from the fused norm kernel, one
 scalar ``all_reduce`` and the fused finalize kernel; nothing synchronises with the host.
 
-ZeRO-3 (parameter partitioning with per-layer gather in forward) is not implemented yet.
+ZeRO-3 (parameter partitioning with per-module gather in forward/backward) is ``zero3.py``.
 """
 
 import contextlib
@@ -120,8 +120,8 @@ class DeepSpeedConfig:
         if isinstance(z, bool):
             z = {"stage": 1 if z else 0}
         self.zero_stage = int(z.get("stage", 0))
-        if self.zero_stage not in (0, 1, 2):
-            raise DeepSpeedConfigError(f"zero_optimization.stage {self.zero_stage} is not supported (0, 1, 2)")
+        if self.zero_stage not in (0, 1, 2, 3):
+            raise DeepSpeedConfigError(f"zero_optimization.stage {self.zero_stage} is not supported (0-3)")
         for k in ("offload_optimizer", "offload_param"):
             dev = (z.get(k) or {}).get("device", "none")
             if dev not in (None, "none"):
@@ -647,22 +647,7 @@ class ZeroEngine(nn.Module):
         self._broadcast_module()
 
         # -- flat spaces -------------------------------------------------------------------
-        by_dtype: Dict[torch.dtype, List[nn.Parameter]] = {}
-        for p in self._params:
-            by_dtype.setdefault(p.dtype, []).append(p)
-        self.spaces: List[_FlatSpace] = []
-        for dt, ps in by_dtype.items():
-            gdt = config.grad_accum_dtype or config.communication_dtype or \
-                (torch.float32 if config.gas > 1 else dt)
-            self.spaces.append(_FlatSpace(ps, dt, gdt, self._shard_world, self._shard_rank,
-                                          config.reduce_bucket_elems, self.device, self._pindex))
-        self._space_of: Dict[int, _FlatSpace] = {}
-        for sp in self.spaces:
-            for b in sp.buckets:
-                for p in b.params:
-                    self._space_of[id(p)] = sp
-            if self.stage == 2:
-                sp.GS = torch.zeros(sp.shard_numel, dtype=sp.grad_dtype, device=self.device)
+        self._build_spaces()
 
         # -- optimizer over fragments ------------------------------------------------------
         master = config.bf16 or any(p.dtype == torch.bfloat16 for p in self._params)
@@ -682,12 +667,7 @@ class ZeroEngine(nn.Module):
             for b in sp.buckets:
                 for li, s, e, boff in b.fragments(self._shard_rank):
                     p = b.params[li]
-                    pv = sp.P.narrow(0, b.start + boff, e - s)
-                    if self.stage == 2:
-                        assert sp.GS is not None
-                        gv = sp.GS.narrow(0, b.shard_off + (boff - self._shard_rank * b.chunk), e - s)
-                    else:
-                        gv = sp.G.narrow(0, b.start + boff, e - s)
+                    pv, gv = self._fragment_views(sp, b, boff, e - s)
                     frag = nn.Parameter(pv, requires_grad=False)
                     if gv.dtype != pv.dtype and hasattr(frag, "grad_dtype"):
                         frag.grad_dtype = None  # fp32-accumulated grads on bf16 weights
@@ -719,9 +699,40 @@ class ZeroEngine(nn.Module):
             lr_scheduler = build_scheduler(config.scheduler, self.optimizer)
         self.lr_scheduler = lr_scheduler
 
-        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(p)) for p in self._params]
+        self._install_hooks()
 
     # -- setup helpers ------------------------------------------------------------------------
+    def _build_spaces(self) -> None:
+        """One flat parameter/gradient space per parameter dtype, cut into reduce buckets."""
+        config = self.config
+        by_dtype: Dict[torch.dtype, List[nn.Parameter]] = {}
+        for p in self._params:
+            by_dtype.setdefault(p.dtype, []).append(p)
+        self.spaces: List[_FlatSpace] = []
+        for dt, ps in by_dtype.items():
+            gdt = config.grad_accum_dtype or config.communication_dtype or \
+                (torch.float32 if config.gas > 1 else dt)
+            self.spaces.append(_FlatSpace(ps, dt, gdt, self._shard_world, self._shard_rank,
+                                          config.reduce_bucket_elems, self.device, self._pindex))
+        self._space_of: Dict[int, _FlatSpace] = {}
+        for sp in self.spaces:
+            for b in sp.buckets:
+                for p in b.params:
+                    self._space_of[id(p)] = sp
+            if self.stage == 2:
+                sp.GS = torch.zeros(sp.shard_numel, dtype=sp.grad_dtype, device=self.device)
+
+    def _fragment_views(self, sp: "_FlatSpace", b: "_Bucket", boff: int, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(parameter view, gradient view) of ``n`` elements at bucket offset ``boff`` of this rank."""
+        pv = sp.P.narrow(0, b.start + boff, n)
+        if self.stage == 2:
+            assert sp.GS is not None
+            return pv, sp.GS.narrow(0, b.shard_off + (boff - self._shard_rank * b.chunk), n)
+        return pv, sp.G.narrow(0, b.start + boff, n)
+
+    def _install_hooks(self) -> None:
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(p)) for p in self._params]
+
     def _broadcast_module(self) -> None:
         if self.world_size <= 1:
             return
@@ -980,8 +991,10 @@ class ZeroEngine(nn.Module):
         tag = tag or f"global_step{self.global_steps}"
         d = os.path.join(os.fspath(save_dir), str(tag))
         os.makedirs(d, exist_ok=True)
+        # stage 3 gathers the partitioned weights with collectives: every rank takes part
+        full_sd = self.state_dict() if self.stage == 3 else None
         if self.global_rank == 0 or (self.dp_rank == 0 and self.process_group is not None):
-            sd = {k: v.detach().to("cpu", copy=True) for k, v in self.module.state_dict().items()}
+            sd = {k: v.detach().to("cpu", copy=True) for k, v in (full_sd or self.state_dict()).items()}
             torch.save({
                 "module": sd,
                 "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler is not None and
@@ -1068,7 +1081,12 @@ def initialize(args: Any = None, model: Optional[nn.Module] = None, optimizer: A
     if optimizer is not None and opt_obj is None and callable(optimizer):
         params = list(model_parameters) if model_parameters is not None else list(model.parameters())
         opt_obj = optimizer(params)
-    engine = ZeroEngine(model, cfg, optimizer=opt_obj, model_parameters=model_parameters, lr_scheduler=lr_scheduler,
+    engine_cls: Any = ZeroEngine
+    if cfg.zero_stage == 3:
+        from determined_amd.parallel.zero3 import Zero3Engine
+
+        engine_cls = Zero3Engine
+    engine = engine_cls(model, cfg, optimizer=opt_obj, model_parameters=model_parameters, lr_scheduler=lr_scheduler,
                         process_group=group, mpu=mpu)
     loader = None
     if training_data is not None:

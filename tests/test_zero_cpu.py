@@ -48,7 +48,7 @@ def _train(rank: int, world: int, stage: int, gas: int, clip: float, bucket: int
             engine.step()
             losses.append(float(loss.detach()))
     assert engine.global_steps == steps and engine.micro_steps == steps * gas
-    return {k: v.clone() for k, v in engine.module.state_dict().items()}
+    return {k: v.clone() for k, v in engine.state_dict().items()}
 
 
 def _reference(world: int, gas: int, clip: float, steps: int = 4):
@@ -78,7 +78,7 @@ def _worker(rank, world, stage, gas, clip, bucket):
 
 
 @pytest.mark.parametrize("stage,gas,clip,bucket", [(2, 1, 0.0, 64), (2, 2, 0.5, 300), (1, 2, 0.0, 10**6),
-                                                   (0, 1, 0.5, 128)])
+                                                   (0, 1, 0.5, 128), (3, 1, 0.0, 64), (3, 2, 0.5, 300)])
 def test_zero_matches_reference(stage, gas, clip, bucket):
     world = 2
     res = run_distributed(_worker, world, args=(stage, gas, clip, bucket))
