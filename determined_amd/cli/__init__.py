@@ -25,7 +25,9 @@ TERMINAL = {"COMPLETED", "CANCELED", "ERROR", "DELETED"}
 
 
 def _session(a: argparse.Namespace) -> Session:
-    return Session(a.master, token=os.environ.get("DET_MASTER_TOKEN"))
+    from determined_amd.cli._iam import stored_token
+
+    return Session(a.master, token=os.environ.get("DET_MASTER_TOKEN") or stored_token(a.master))
 
 
 def _print(rows: List[Dict[str, Any]], cols: List[str], a: argparse.Namespace) -> None:
@@ -512,6 +514,11 @@ def build_parser() -> argparse.ArgumentParser:
     wc.add_argument("--trigger", action="append")
     wc.set_defaults(fn=webhook_create)
     wh.add_parser("list").set_defaults(fn=webhook_list)
+
+    from determined_amd.cli import _iam
+
+    _iam.register(sub, _session, _print)
+    _iam.register_experiment_move(e, _session)
 
     dp = sub.add_parser("deploy").add_subparsers(dest="where", required=True)
     loc = dp.add_parser("local").add_subparsers(dest="verb", required=True)

@@ -20,6 +20,8 @@ def main(argv=None) -> int:
     p.add_argument("--fit", choices=["best", "worst"], default=None)
     p.add_argument("--no-preemption", action="store_true")
     p.add_argument("--auth-token", default=os.environ.get("DET_MASTER_TOKEN"))
+    p.add_argument("--auth", choices=["none", "basic", "rbac"], default=None,
+                   help="user authentication / authorization mode (default none: single-user node)")
     a = p.parse_args(argv)
     cfg = {}
     if a.config_file:
@@ -33,7 +35,8 @@ def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     m = Master(db_path=db, policy=a.scheduler or cfg.get("scheduler", "priority"), fit=a.fit or cfg.get("fit", "best"),
                preemption=not a.no_preemption and cfg.get("preemption", True),
-               master_url=cfg.get("advertised_url", f"http://{host}:{port}"), auth_token=a.auth_token)
+               master_url=cfg.get("advertised_url", f"http://{host}:{port}"), auth_token=a.auth_token,
+               auth=a.auth or cfg.get("auth", "none"))
     srv = MasterServer(m, host, port)
     logging.getLogger("determined_amd.master").info(f"master listening on http://{host}:{srv.port}")
     try:

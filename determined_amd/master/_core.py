@@ -88,13 +88,15 @@ class ExperimentRec:
 class Master:
     def __init__(self, db_path: str = ":memory:", policy: str = "priority", fit: str = "best",
                  preemption: bool = True, cluster_id: Optional[str] = None, master_url: str = "http://127.0.0.1:8080",
-                 auth_token: Optional[str] = None) -> None:
+                 auth_token: Optional[str] = None, auth: str = "none") -> None:
         from determined_amd._native import load
+        from determined_amd.master._iam import IAM
 
         self.native = load()
         self.lock = threading.RLock()
         self.cv = threading.Condition(self.lock)
         self.db = DB(db_path)
+        self.iam = IAM(self.db, mode=auth, cluster_token=auth_token)
         pol = {"priority": self.native.Policy.PRIORITY, "fair_share": self.native.Policy.FAIR_SHARE,
                "round_robin": self.native.Policy.ROUND_ROBIN}[policy]
         self.policy = policy
@@ -175,7 +177,8 @@ class Master:
                                  config=cfg, model_def=model_def, parent_id=parent_id, start_time=time.time(),
                                  description=cfg.get("description") or "", labels=cfg.get("labels") or [],
                                  unmanaged=int(unmanaged), project=cfg.get("project") or "Uncategorized",
-                                 workspace=cfg.get("workspace") or "Uncategorized")
+                                 workspace=cfg.get("workspace") or "Uncategorized",
+                                 owner=self.iam.current()["username"])
             exp = ExperimentRec(eid, cfg, "ACTIVE" if activate else "PAUSED")
             self.experiments[eid] = exp
             if cfg["searcher"]["name"] == "custom":

@@ -17,6 +17,8 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from determined_amd import __version__
 from determined_amd.config import InvalidConfig
+from determined_amd.master._iam import AuthError, _public_user
+from determined_amd.master._iam_routes import add_iam_routes
 from determined_amd.master._core import Master
 
 logger = logging.getLogger("determined_amd.master")
@@ -29,6 +31,15 @@ class HTTPError(Exception):
         super().__init__(message)
         self.status = status
         self.message = message
+
+
+def _guard_exp(m: Master, eid: Any, perm: str) -> Dict[str, Any]:
+    row = m.db.one("SELECT id, owner, workspace FROM experiments WHERE id=?", [int(eid)])
+    if row is None:
+        raise HTTPError(404, f"experiment {eid} not found")
+    sc = m.iam.experiment_scope(row)
+    m.iam.require(perm, sc["workspace_id"], sc["owner_id"])
+    return row
 
 
 def _exp_summary(m: Master, row: Dict[str, Any]) -> Dict[str, Any]:
@@ -78,16 +89,20 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("GET", "/api/v1/me")
     def me(q, b):
-        return {"user": {"username": "determined", "admin": True}}
+        return {"user": _public_user(m.iam.current())}
 
     @route("POST", "/api/v1/auth/login")
     def login(q, b):
-        return {"token": m.auth_token or "", "user": {"username": b.get("username", "determined")}}
+        return m.iam.login(b.get("username", "determined"), b.get("password", ""))
+
+    add_iam_routes(route, m)
 
     # ---------------------------------------------------------------- experiments
     @route("POST", "/api/v1/experiments")
     def create_exp(q, b):
         md = base64.b64decode(b["model_def"]) if b.get("model_def") else None
+        cfg0 = b["config"] if isinstance(b.get("config"), dict) else {}
+        m.iam.resolve_target(cfg0)
         try:
             eid = m.create_experiment(b["config"], md, activate=b.get("activate", True),
                                       parent_id=b.get("parent_id"), unmanaged=bool(b.get("unmanaged")))
@@ -115,6 +130,12 @@ def build_routes(m: Master) -> List[Route]:
     @route("GET", "/api/v1/experiments")
     def list_exps(q, b):
         rows = m.db.all("SELECT * FROM experiments WHERE state!='DELETED' ORDER BY id")
+        if q.get("workspace"):
+            rows = [r for r in rows if r.get("workspace") == q["workspace"]]
+        if q.get("project"):
+            rows = [r for r in rows if r.get("project") == q["project"]]
+        if q.get("user"):
+            rows = [r for r in rows if r.get("owner") == q["user"]]
         if q.get("archived") in ("false", "0"):
             rows = [r for r in rows if not r["archived"]]
         return {"experiments": [_exp_summary(m, r) for r in rows]}
@@ -138,6 +159,7 @@ def build_routes(m: Master) -> List[Route]:
                             ("kill", "kill_experiment"), ("cancel", "kill_experiment")):
         def make(fn_name=fn_name):
             def handler(q, b, eid):
+                _guard_exp(m, eid, "edit")
                 getattr(m, fn_name)(int(eid))
                 return {}
             return handler
@@ -146,16 +168,19 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("POST", r"/api/v1/experiments/(\d+)/archive")
     def archive(q, b, eid):
+        _guard_exp(m, eid, "edit")
         m.archive_experiment(int(eid), True)
         return {}
 
     @route("POST", r"/api/v1/experiments/(\d+)/unarchive")
     def unarchive(q, b, eid):
+        _guard_exp(m, eid, "edit")
         m.archive_experiment(int(eid), False)
         return {}
 
     @route("DELETE", r"/api/v1/experiments/(\d+)")
     def delete_exp(q, b, eid):
+        _guard_exp(m, eid, "edit")
         try:
             m.delete_experiment(int(eid))
         except ValueError as e:
@@ -164,6 +189,7 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("PATCH", r"/api/v1/experiments/(\d+)")
     def patch_exp(q, b, eid):
+        _guard_exp(m, eid, "edit")
         cols = {k: v for k, v in b.items() if k in ("name", "description", "notes", "labels")}
         m.db.update("experiments", "id", int(eid), **cols)
         return {}
@@ -373,6 +399,7 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("POST", r"/api/v1/agents/([^/]+)/(enable|disable)")
     def agent_enable(q, b, agent_id, what):
+        m.iam.require("admin_cluster")
         with m.lock:
             if agent_id in m.agents:
                 m.agents[agent_id]["enabled"] = what == "enable"
@@ -536,10 +563,14 @@ class _Handler(BaseHTTPRequestHandler):
         raw = self.rfile.read(n) if n else b""
         status, ctype = 200, "application/json"
         try:
-            tok = self.master.auth_token if self.master else None
-            if tok and parsed.path.startswith("/api/") and not parsed.path.startswith("/api/v1/auth") and \
-                    self.headers.get("Authorization") != f"Bearer {tok}":
-                raise HTTPError(401, "unauthenticated")
+            iam = self.master.iam if self.master else None
+            if iam is not None:
+                iam.set_current(None)
+                if parsed.path.startswith("/api/") and parsed.path != "/api/v1/auth/login":
+                    try:
+                        iam.set_current(iam.authenticate(self.headers.get("Authorization")))
+                    except AuthError as e:
+                        raise HTTPError(e.status, e.message)
             body = json.loads(raw) if raw else {}
             for meth, pat, fn in self.routes:
                 if meth != method:
@@ -554,7 +585,7 @@ class _Handler(BaseHTTPRequestHandler):
                 data, ctype = out.body.encode(), out.ctype
             else:
                 data = json.dumps(out, default=str).encode()
-        except HTTPError as e:
+        except (HTTPError, AuthError) as e:
             status, data = e.status, json.dumps({"error": e.message}).encode()
         except KeyError as e:
             status, data = 404, json.dumps({"error": str(e)}).encode()
