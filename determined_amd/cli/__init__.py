@@ -478,7 +478,15 @@ def build_parser() -> argparse.ArgumentParser:
     mr.add_argument("uuid")
     mr.set_defaults(fn=model_register)
 
-    sub.add_parser("master").add_subparsers(dest="verb", required=True).add_parser("info").set_defaults(fn=master_info)
+    from determined_amd.cli import _ntsc
+
+    master_fns = _ntsc.register(sub, _session, _print, _follow_logs)
+    ms = sub.add_parser("master").add_subparsers(dest="verb", required=True)
+    ms.add_parser("info").set_defaults(fn=master_info)
+    ms.add_parser("config").set_defaults(fn=master_fns["config"])
+    ml = ms.add_parser("logs")
+    ml.add_argument("--tail", type=int, default=200)
+    ml.set_defaults(fn=master_fns["logs"])
     sub.add_parser("agent", aliases=["a"]).add_subparsers(dest="verb", required=True).add_parser(
         "list").set_defaults(fn=agent_list)
     sub.add_parser("slot", aliases=["s"]).add_subparsers(dest="verb", required=True).add_parser(
@@ -489,6 +497,11 @@ def build_parser() -> argparse.ArgumentParser:
         "list").set_defaults(fn=job_list)
 
     cm = sub.add_parser("command", aliases=["cmd"]).add_subparsers(dest="verb", required=True)
+    cm.add_parser("list").set_defaults(fn=lambda a: _print(_session(a).get("/api/v1/commands")["tasks"],
+                                                           ["id", "type", "state", "exit_code"], a))
+    ck_ = cm.add_parser("kill")
+    ck_.add_argument("task_id")
+    ck_.set_defaults(fn=lambda a: _session(a).post(f"/api/v1/tasks/{a.task_id}/kill", {}))
     cr = cm.add_parser("run")
     cr.add_argument("cmd", nargs=argparse.REMAINDER)
     cr.add_argument("--slots", type=int, default=0)

@@ -9,6 +9,7 @@ the native scheduler; allocations are dispatched to agents, which launch the har
 
 import base64
 import json
+import re
 import logging
 import os
 import threading
@@ -100,6 +101,7 @@ class Master:
         pol = {"priority": self.native.Policy.PRIORITY, "fair_share": self.native.Policy.FAIR_SHARE,
                "round_robin": self.native.Policy.ROUND_ROBIN}[policy]
         self.policy = policy
+        self.fit = fit
         self.sched = self.native.Scheduler(pol, self.native.Fit.BEST if fit == "best" else self.native.Fit.WORST,
                                            preemption)
         self.cluster_id = cluster_id or str(uuid.uuid4())
@@ -523,6 +525,7 @@ class Master:
                 "DET_MASTER": self.master_url,
                 "DET_CLUSTER_ID": self.cluster_id,
                 "DET_AGENT_ID": agent_id,
+                "DET_AGENT_HOST": ag.get("host", "127.0.0.1"),
                 "DET_ALLOCATION_ID": a.id,
                 "DET_TASK_ID": a.task_id,
                 "DET_SESSION_TOKEN": self.auth_token or "",
@@ -785,7 +788,24 @@ class Master:
                 "INSERT INTO task_logs (task_id, allocation_id, rank, ts, log) VALUES (?,?,?,?,?)",
                 [(task_id, allocation_id, l.get("rank"), now, l["log"]) for l in logs])
             self._apply_log_policies(task_id, allocation_id, logs)
+            self._log_webhooks(task_id, logs)
             self.cv.notify_all()
+
+    def _log_webhooks(self, task_id: str, logs: List[Dict[str, Any]]) -> None:
+        if not task_id.startswith("trial-"):
+            return
+        hooks = self.db.all("SELECT triggers FROM webhooks")
+        rxs = [t["condition"]["regex"] for h in hooks for t in (h.get("triggers") or [])
+               if isinstance(t, dict) and t.get("trigger_type") == "TASK_LOG" and (t.get("condition") or {}).get("regex")]
+        if not rxs:
+            return
+        try:
+            exp, tr = self._trial(int(task_id.split("-", 1)[1]))
+        except (KeyError, ValueError):
+            return
+        for l in logs:
+            if any(re.search(rx, l.get("log", "")) for rx in rxs):
+                self._fire_webhooks(exp, "TASK_LOG", tr, log_line=l.get("log", ""))
 
     def _apply_log_policies(self, task_id: str, allocation_id: Optional[str], logs: List[Dict[str, Any]]) -> None:
         """Experiment ``log_policies`` (reference ``master/internal/logpattern``): a regex match in a
@@ -937,24 +957,63 @@ class Master:
             self.db.update("checkpoints", "uuid", u, state="DELETED")
 
     # ================================================================ webhooks
-    def _fire_webhooks(self, exp: ExperimentRec, trigger: str, trial: Optional[TrialRec] = None) -> None:
+    def _fire_webhooks(self, exp: ExperimentRec, trigger: str, trial: Optional[TrialRec] = None,
+                       log_line: Optional[str] = None) -> None:
+        """POST an event to every matching webhook (reference ``master/internal/webhooks``).
+
+        Triggers: ``EXPERIMENT_STATE_CHANGE`` (``condition: {"state": S}`` narrows it) and
+        ``TASK_LOG`` (``condition: {"regex": R}`` over trial log lines).  ``webhook_type``
+        ``SLACK`` posts a Slack ``{"blocks": ...}`` message, ``DEFAULT`` the JSON event.  Every
+        request is signed: ``X-Determined-AMD-Signature: sha256=<hmac(timestamp.body)>`` with
+        the master's webhook secret (cluster id) and ``X-Determined-AMD-Timestamp``."""
         hooks = self.db.all("SELECT * FROM webhooks")
         if not hooks:
             return
-        payload = {"event_type": trigger, "experiment": {"id": exp.id, "state": exp.state,
-                                                         "name": exp.config.get("name")}}
+        payload: Dict[str, Any] = {"event_type": trigger, "timestamp": int(time.time()),
+                                   "experiment": {"id": exp.id, "state": exp.state, "name": exp.config.get("name"),
+                                                  "workspace": exp.config.get("workspace") or "Uncategorized",
+                                                  "project": exp.config.get("project") or "Uncategorized"}}
         if trial is not None:
             payload["trial"] = {"id": trial.id, "state": trial.state}
+        if log_line is not None:
+            payload["log"] = log_line
+        targets = []
+        for h in hooks:
+            for t in h.get("triggers") or [{"trigger_type": "EXPERIMENT_STATE_CHANGE"}]:
+                tt = t.get("trigger_type", t) if isinstance(t, dict) else t
+                cond = (t.get("condition") or {}) if isinstance(t, dict) else {}
+                if tt != trigger:
+                    continue
+                if trigger == "EXPERIMENT_STATE_CHANGE" and cond.get("state") and cond["state"] != exp.state:
+                    continue
+                if trigger == "TASK_LOG" and cond.get("regex") and not re.search(cond["regex"], log_line or ""):
+                    continue
+                targets.append(h)
+                break
+        if not targets:
+            return
+        secret = self.cluster_id.encode()
 
         def send() -> None:
+            import hashlib
+            import hmac
+
             import requests
 
-            for h in hooks:
-                trig = h.get("triggers") or []
-                if trig and trigger not in [t.get("trigger_type", t) if isinstance(t, dict) else t for t in trig]:
-                    continue
+            for h in targets:
+                if h.get("webhook_type") == "SLACK":
+                    text = f"Experiment {exp.id} ({exp.config.get('name')}): {trigger} -> {exp.state}"
+                    if log_line is not None:
+                        text += f"\n`{log_line}`"
+                    body = json.dumps({"blocks": [{"type": "section", "text": {"type": "mrkdwn", "text": text}}]})
+                else:
+                    body = json.dumps(payload)
+                ts = str(payload["timestamp"])
+                sig = hmac.new(secret, (ts + "." + body).encode(), hashlib.sha256).hexdigest()
                 try:
-                    requests.post(h["url"], json=payload, timeout=5)
+                    requests.post(h["url"], data=body, timeout=5, headers={
+                        "Content-Type": "application/json", "X-Determined-AMD-Timestamp": ts,
+                        "X-Determined-AMD-Signature": f"sha256={sig}"})
                 except Exception as e:
                     logger.debug(f"webhook {h['url']} failed: {e}")
 

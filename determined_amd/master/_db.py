@@ -46,10 +46,10 @@ CREATE TABLE IF NOT EXISTS webhooks (
 CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
 """
 
-MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT")]
+MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT")]
 
 JSON_COLS = {"config", "hparams", "metrics", "batch_metrics", "resources", "metadata", "searcher_snapshot", "labels",
-             "searcher_state", "triggers"}
+             "searcher_state", "triggers", "proxy"}
 
 
 class DB:

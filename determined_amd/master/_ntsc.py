@@ -1,0 +1,100 @@
+"""Notebooks, shells, TensorBoards and commands ("NTSC" tasks) plus master config/log routes
+(reference: ``master/internal/command/*``, ``api_notebook.go``, ``api_shell.go``,
+``api_tensorboard.go``, ``api_command.go``, ``api_master.go`` GetMasterConfig / MasterLogs).
+
+Every NTSC task is a generic command allocation (``Master.create_command``) whose entrypoint is
+one of the ``determined_amd.exec`` task programs; once running, a task reports where it lives
+(``POST /api/v1/tasks/<id>/proxy``) and the CLI reads that back.
+"""
+
+import collections
+import logging
+import secrets
+import sys
+import time
+from typing import Any, Callable, Deque, Dict, List
+
+KINDS = {"notebooks": "NOTEBOOK", "shells": "SHELL", "tensorboards": "TENSORBOARD", "commands": "COMMAND"}
+
+
+class _RingHandler(logging.Handler):
+    """Keeps the master's last log records for ``GET /api/v1/master/logs``."""
+
+    def __init__(self, cap: int = 5000) -> None:
+        super().__init__(logging.INFO)
+        self.records: Deque[Dict[str, Any]] = collections.deque(maxlen=cap)
+        self.seq = 0
+
+    def emit(self, record: logging.LogRecord) -> None:
+        self.seq += 1
+        self.records.append({"id": self.seq, "ts": record.created, "level": record.levelname,
+                             "logger": record.name, "message": record.getMessage()})
+
+
+_RING = _RingHandler()
+logging.getLogger("determined_amd").addHandler(_RING)
+
+
+def task_command(kind: str, b: Dict[str, Any]) -> List[str]:
+    py = [sys.executable, "-m"]
+    if kind == "TENSORBOARD":
+        ids = ",".join(str(int(x)) for x in b.get("experiment_ids") or [])
+        tids = ",".join(str(int(x)) for x in b.get("trial_ids") or [])
+        if not ids and not tids:
+            raise ValueError("a tensorboard needs experiment_ids or trial_ids")
+        return py + ["determined_amd.exec.tensorboard", "--experiment-ids", ids, "--trial-ids", tids]
+    if kind == "SHELL":
+        return py + ["determined_amd.exec.shell", "--idle-timeout", str(float(b.get("idle_timeout", 0)))]
+    if kind == "NOTEBOOK":
+        return py + ["determined_amd.exec.notebook"]
+    cmd = b.get("command") or b.get("entrypoint")
+    if not cmd:
+        raise ValueError("a command needs 'command'")
+    return cmd
+
+
+def add_ntsc_routes(route: Callable[[str, str], Callable], m: Any) -> None:
+    for plural, kind in KINDS.items():
+        if kind == "COMMAND":
+            continue  # POST /api/v1/commands is the generic route in _server
+
+        def make_create(kind=kind):
+            def create(q, b):
+                env = dict(b.get("env") or {})
+                if kind == "NOTEBOOK":
+                    env["DET_NOTEBOOK_TOKEN"] = secrets.token_hex(16)
+                try:
+                    cmd = task_command(kind, b)
+                except ValueError as e:
+                    from determined_amd.master._server import HTTPError
+
+                    raise HTTPError(400, str(e))
+                tid = m.create_command(cmd, int(b.get("slots", 0)), env, kind, b.get("workdir_b64"))
+                return {"task_id": tid, "type": kind}
+            return create
+
+        route("POST", f"/api/v1/{plural}")(make_create())
+
+    for plural, kind in KINDS.items():
+        def make_list(kind=kind):
+            def lst(q, b):
+                rows = m.db.all("SELECT * FROM tasks WHERE type=? ORDER BY start_time", [kind])
+                return {"tasks": rows}
+            return lst
+
+        route("GET", f"/api/v1/{plural}")(make_list())
+
+    @route("GET", "/api/v1/master/config")
+    def master_config(q, b):
+        m.iam.require("view")
+        return {"config": {"scheduler": {"type": m.policy, "fitting_policy": getattr(m, "fit", None)},
+                           "auth": m.iam.mode, "master_url": m.master_url, "cluster_id": m.cluster_id,
+                           "db": m.db.path, "log_retention_days": None}}
+
+    @route("GET", "/api/v1/master/logs")
+    def master_logs(q, b):
+        m.iam.require("admin_cluster")
+        after = int(q.get("after", 0))
+        limit = int(q.get("limit", 1000))
+        recs = [r for r in list(_RING.records) if r["id"] > after]
+        return {"logs": recs[-limit:], "now": time.time()}

@@ -19,6 +19,7 @@ from determined_amd import __version__
 from determined_amd.config import InvalidConfig
 from determined_amd.master._iam import AuthError, _public_user
 from determined_amd.master._iam_routes import add_iam_routes
+from determined_amd.master._ntsc import add_ntsc_routes
 from determined_amd.master._core import Master
 
 logger = logging.getLogger("determined_amd.master")
@@ -351,6 +352,15 @@ def build_routes(m: Master) -> List[Route]:
         tid = m.create_command(b["command"], int(b.get("slots", 0)), b.get("env"), b.get("type", "COMMAND"),
                                b.get("workdir_b64"))
         return {"task_id": tid}
+
+    @route("POST", r"/api/v1/tasks/([^/]+)/proxy")
+    def task_proxy(q, b, task_id):
+        if m.db.one("SELECT id FROM tasks WHERE id=?", [task_id]) is None:
+            raise HTTPError(404, f"task {task_id} not found")
+        m.db.update("tasks", "id", task_id, proxy={k: b.get(k) for k in ("host", "port", "cwd", "env")})
+        return {}
+
+    add_ntsc_routes(route, m)
 
     @route("GET", "/api/v1/tasks")
     def list_tasks(q, b):
