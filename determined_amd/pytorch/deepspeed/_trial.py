@@ -61,6 +61,11 @@ class DeepSpeedTrialController(_PyTorchTrialController):
                                              "wrapping your model with wrap_model_engine()")
         super().__init__(trial_inst, context, **kw)
         self.context: DeepSpeedTrialContext = context
+        # DeepSpeed autotuning profiling run (``pytorch/dsat``): time a window of batches and
+        # report throughput/latency instead of validating; OOM -> InvalidHP (early exit)
+        self._dsat: Optional[Dict[str, Any]] = (context.get_hparams() or {}).get("_dsat_mode") or None
+        self._dsat_t0: Optional[float] = None
+        self._dsat_t1: Optional[float] = None
 
     # -- data ------------------------------------------------------------------------------------
     def _set_data_loaders(self) -> None:
@@ -117,6 +122,55 @@ class DeepSpeedTrialController(_PyTorchTrialController):
 
     # -- train -----------------------------------------------------------------------------------
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
+        if self._dsat is None:
+            return self._train_batch_inner(batch, epoch_idx, batch_idx)
+        import time
+
+        start, end = int(self._dsat["start_profile_step"]), int(self._dsat["end_profile_step"])
+        try:
+            if batch_idx == start:
+                self._sync_device()
+                self._dsat_t0 = time.perf_counter()
+            out = self._train_batch_inner(batch, epoch_idx, batch_idx)
+            if batch_idx + 1 == end:
+                self._sync_device()
+                self._dsat_t1 = time.perf_counter()
+            return out
+        except torch.OutOfMemoryError as e:
+            raise core.InvalidHP(f"dsat: out of memory at micro-batch "
+                                 f"{self.context.train_micro_batch_size_per_gpu}: {e}") from None
+        except RuntimeError as e:
+            if "out of memory" in str(e).lower():
+                raise core.InvalidHP(f"dsat: out of memory: {e}") from None
+            raise
+
+    def _sync_device(self) -> None:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def _validate(self, op: Any = None) -> Dict[str, Any]:
+        if self._dsat is None:
+            return super()._validate(op)
+        start, end = int(self._dsat["start_profile_step"]), int(self._dsat["end_profile_step"])
+        if self._dsat_t0 is None or self._dsat_t1 is None or self.state.batches_trained < end:
+            self.state.last_val = self.state.batches_trained
+            return {}
+        dt = max(self._dsat_t1 - self._dsat_t0, 1e-9)
+        ctx = self.context
+        samples = (end - start) * ctx.train_micro_batch_size_per_gpu * ctx.num_micro_batches_per_slot
+        dts = [x for x in ctx.distributed.allgather(dt)]
+        dt = max(dts)  # the slowest rank bounds the step
+        metrics = {"throughput": samples / dt, "latency": dt / (end - start),
+                   "train_micro_batch_size_per_gpu": ctx.train_micro_batch_size_per_gpu,
+                   "zero_stage": int(getattr(ctx.models[0], "stage", -1))}
+        self.state.last_val = self.state.batches_trained
+        if self.is_chief:
+            self.core_context.train.report_validation_metrics(self.state.batches_trained, metrics)
+            if op is not None and not op._completed:
+                op.report_completed(float(metrics[self._dsat.get("metric", "throughput")]))
+        return metrics
+
+    def _train_batch_inner(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
         ctx = self.context
         calls = 1 if (ctx.use_pipeline_parallel or ctx._manual_grad_accumulation) else ctx.num_micro_batches_per_slot
         per_micro: List[Dict[str, Any]] = []
@@ -168,6 +222,9 @@ class DeepSpeedTrialController(_PyTorchTrialController):
 
     # -- checkpoint ------------------------------------------------------------------------------
     def _checkpoint(self, already_exiting: bool) -> None:
+        if self._dsat is not None:  # profiling runs never checkpoint
+            self.state.last_ckpt = self.state.batches_trained
+            return
         if self.is_chief:
             self.core_context.train.set_status("checkpointing")
         self.state.last_ckpt = self.state.batches_trained
