@@ -33,7 +33,7 @@ ARCH = os.environ.get("DAMD_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip"]
 HOST_SOURCES = ["bindings.cpp"]
-NATIVE_SOURCES = ["searcher.cpp", "scheduler.cpp", "module.cpp"]
+NATIVE_SOURCES = ["searcher.cpp", "scheduler.cpp", "loader.cpp", "module.cpp"]
 
 
 def _ext_suffix() -> str:
@@ -128,13 +128,13 @@ def build_native(force: bool = False, jobs: int = 8) -> pathlib.Path:
         o = BUILD / ("native_" + s.name + ".o")
         objs.append(o)
         if force or _newer(o, [s] + headers):
-            jobs_list.append([CXX, "-O2", "-fPIC", "-std=c++17", "-Wall", f"-I{pybind11.get_include()}",
+            jobs_list.append([CXX, "-O3", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
                               f"-I{py_inc}", f"-I{src_dir}", "-c", str(s), "-o", str(o)])
     with concurrent.futures.ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, jobs_list))
     out = native_path()
     if objs and (force or jobs_list or _newer(out, objs)):
-        _run([CXX, "-shared", *map(str, objs), "-o", str(out)])
+        _run([CXX, "-shared", "-pthread", *map(str, objs), "-o", str(out)])
     return out
 
 

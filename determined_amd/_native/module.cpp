@@ -181,7 +181,12 @@ py::dict request_to_py(const Request& r) {
 
 }  // namespace
 
+namespace damd_native {
+void register_loader(py::module& m);
+}
+
 PYBIND11_MODULE(_native, m) {
+  damd_native::register_loader(m);
   m.doc() = "determined_amd native control plane: search methods + scheduler";
   py::class_<SearchEngine>(m, "SearchEngine")
       .def(py::init<const py::dict&, const py::list&, uint64_t>(), py::arg("config"), py::arg("hparams"),
