@@ -835,17 +835,23 @@ class ZeroEngine(nn.Module):
         return (self.micro_steps + 1) % self.config.gas == 0
 
     def backward(self, loss: torch.Tensor, retain_graph: bool = False, scale_wrt_gas: bool = True) -> torch.Tensor:
+        self.begin_micro_backward()
+        if scale_wrt_gas and self.config.gas > 1:
+            loss = loss / self.config.gas
+        loss.backward(retain_graph=retain_graph)
+        self._end_backward()
+        return loss
+
+    def begin_micro_backward(self) -> None:
+        """Bracket a micro-batch backward that is not driven through ``backward(loss)`` (the
+        pipeline engine back-propagates a received output gradient): call this before, and
+        ``_end_backward()`` after, ``torch.autograd.backward``."""
         self._wait_gather()
         self._boundary_now = self.is_gradient_accumulation_boundary()
         if self.micro_steps % self.config.gas == 0:  # first micro-batch of a window: overwrite G
             for sp in self.spaces:
                 for b in sp.buckets:
                     b.touched = [False] * len(b.params)
-        if scale_wrt_gas and self.config.gas > 1:
-            loss = loss / self.config.gas
-        loss.backward(retain_graph=retain_graph)
-        self._end_backward()
-        return loss
 
     @contextlib.contextmanager
     def no_sync(self) -> Iterator[None]:
@@ -1074,6 +1080,10 @@ def initialize(args: Any = None, model: Optional[nn.Module] = None, optimizer: A
         raise DeepSpeedConfigError("initialize() requires a DeepSpeed config (config=dict or path)")
     group = mpu.get_data_parallel_group() if mpu is not None and hasattr(mpu, "get_data_parallel_group") else None
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    from determined_amd.parallel.pipeline import PipelineEngine, PipelineModule
+
+    if isinstance(model, PipelineModule):
+        world = max(1, world // model.num_stages)  # batch sizes count data-parallel replicas only
     cfg = DeepSpeedConfig(config, world)
     if isinstance(optimizer, dict):
         cfg.optimizer, optimizer = optimizer, None
@@ -1081,6 +1091,10 @@ def initialize(args: Any = None, model: Optional[nn.Module] = None, optimizer: A
     if optimizer is not None and opt_obj is None and callable(optimizer):
         params = list(model_parameters) if model_parameters is not None else list(model.parameters())
         opt_obj = optimizer(params)
+    if isinstance(model, PipelineModule):
+        pe = PipelineEngine(model, cfg, optimizer=opt_obj, model_parameters=model_parameters,
+                            lr_scheduler=lr_scheduler)
+        return pe, pe.optimizer, None, pe.lr_scheduler
     engine_cls: Any = ZeroEngine
     if cfg.zero_stage == 3:
         from determined_amd.parallel.zero3 import Zero3Engine
