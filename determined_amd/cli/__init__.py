@@ -493,8 +493,8 @@ def build_parser() -> argparse.ArgumentParser:
         "list").set_defaults(fn=slot_list)
     sub.add_parser("resource-pool", aliases=["rp"]).add_subparsers(dest="verb", required=True).add_parser(
         "list").set_defaults(fn=pool_list)
-    sub.add_parser("job", aliases=["j"]).add_subparsers(dest="verb", required=True).add_parser(
-        "list").set_defaults(fn=job_list)
+    jb = sub.add_parser("job", aliases=["j"]).add_subparsers(dest="verb", required=True)
+    jb.add_parser("list").set_defaults(fn=job_list)
 
     cm = sub.add_parser("command", aliases=["cmd"]).add_subparsers(dest="verb", required=True)
     cm.add_parser("list").set_defaults(fn=lambda a: _print(_session(a).get("/api/v1/commands")["tasks"],
@@ -514,7 +514,12 @@ def build_parser() -> argparse.ArgumentParser:
     tlg.add_argument("task_id")
     tlg.set_defaults(fn=task_logs)
 
+    from determined_amd.cli import _extra
+
+    _extra.register({"experiment": e, "trial": t, "model": mo, "job": jb, "task": tk2}, _session, _print)
+
     tp = sub.add_parser("template", aliases=["tpl"]).add_subparsers(dest="verb", required=True)
+    _extra.register_template(tp, _session)
     ts = tp.add_parser("set")
     ts.add_argument("name")
     ts.add_argument("file")

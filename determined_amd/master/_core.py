@@ -75,6 +75,7 @@ class TrialRec:
 
 class ExperimentRec:
     def __init__(self, eid: int, cfg: Dict[str, Any], state: str) -> None:
+        self.deferred: List["TrialRec"] = []  # trials waiting for resources.max_slots
         self.id = eid
         self.config = cfg
         self.state = state
@@ -446,8 +447,30 @@ class Master:
         self._order += 1
         return self._order
 
+    def _exp_slots_in_use(self, exp: ExperimentRec) -> int:
+        return sum(a.slots for a in self.allocations.values() if a.exp_id == exp.id and a.state != "TERMINATED")
+
     def _request_allocation(self, exp: ExperimentRec, tr: TrialRec) -> None:
         slots = int(exp.config["resources"].get("slots_per_trial", 1))
+        cap = exp.config["resources"].get("max_slots")
+        if cap is not None and self._exp_slots_in_use(exp) + slots > int(cap):
+            # resources.max_slots: queue the trial in the master until the experiment frees slots
+            if tr not in exp.deferred:
+                exp.deferred.append(tr)
+            return
+        self._start_request(exp, tr, slots)
+
+    def _drain_deferred(self, exp: ExperimentRec) -> None:
+        cap = exp.config["resources"].get("max_slots")
+        slots = int(exp.config["resources"].get("slots_per_trial", 1))
+        while exp.deferred and exp.state == "ACTIVE":
+            if cap is not None and self._exp_slots_in_use(exp) + slots > int(cap):
+                return
+            tr = exp.deferred.pop(0)
+            if tr.state not in TERMINAL_TRIAL and tr.allocation is None:
+                self._start_request(exp, tr, slots)
+
+    def _start_request(self, exp: ExperimentRec, tr: TrialRec, slots: int) -> None:
         aid = f"trial-{tr.id}.{tr.run_id + 1}.{uuid.uuid4().hex[:6]}"
         a = Allocation(aid, f"trial-{tr.id}", slots, exp.id, tr.id)
         tr.allocation = a
@@ -477,7 +500,74 @@ class Master:
     def _drop_allocation(self, a: Allocation) -> None:
         self.sched.remove_request(a.id)
         a.state = "TERMINATED"
+        if a.exp_id is not None and a.exp_id in self.experiments:
+            exp = self.experiments[a.exp_id]
+            if exp.deferred:
+                self._drain_deferred(exp)
         self.cv.notify_all()
+
+    # ================================================================ experiment settings
+    def set_experiment_resources(self, eid: int, max_slots: Any = "unset", weight: Optional[float] = None,
+                                 priority: Optional[int] = None) -> None:
+        """``det experiment set max-slots|weight|priority`` / job-queue updates."""
+        with self.lock:
+            exp = self._exp(eid)
+            res = exp.config.setdefault("resources", {})
+            if max_slots != "unset":
+                res["max_slots"] = None if max_slots is None else int(max_slots)
+            if weight is not None:
+                res["weight"] = float(weight)
+                self.sched.set_weight(f"exp-{eid}", float(weight))
+            if priority is not None:
+                res["priority"] = int(priority)
+                self.sched.set_priority(f"exp-{eid}", int(priority))
+            self.db.update("experiments", "id", eid, config=exp.config)
+            self._drain_deferred(exp)
+            self.cv.notify_all()
+
+    def patch_experiment_config(self, eid: int, section: str, values: Dict[str, Any]) -> Dict[str, Any]:
+        """Update a mutable config section (checkpoint_storage GC policy, retention_policy)."""
+        if section not in ("checkpoint_storage", "retention_policy"):
+            raise ValueError(f"config section {section!r} is not mutable")
+        with self.lock:
+            row = self.db.one("SELECT config FROM experiments WHERE id=?", [eid])
+            if row is None:
+                raise KeyError(f"experiment {eid} not found")
+            cfg = row["config"]
+            sec = dict(cfg.get(section) or {})
+            sec.update(values)
+            cfg[section] = sec
+            self.db.update("experiments", "id", eid, config=cfg)
+            if eid in self.experiments:
+                self.experiments[eid].config = cfg
+            return cfg
+
+    def continue_experiment(self, eid: int, overrides: Optional[Dict[str, Any]] = None) -> int:
+        """``det experiment continue``: a new single-trial experiment warm-started from the
+        parent's latest (or best) checkpoint, same model definition."""
+        import copy
+
+        row = self.db.one("SELECT * FROM experiments WHERE id=?", [eid])
+        if row is None:
+            raise KeyError(f"experiment {eid} not found")
+        trials = self.db.all("SELECT id, hparams, latest_checkpoint FROM trials WHERE experiment_id=? ORDER BY id",
+                             [eid])
+        if len(trials) != 1:
+            raise ValueError("continue needs an experiment with exactly one trial")
+        ck = trials[0]["latest_checkpoint"]
+        cfg = copy.deepcopy(row["config"])
+        for k, v in (overrides or {}).items():
+            cur = cfg
+            parts = k.split(".")
+            for p in parts[:-1]:
+                cur = cur.setdefault(p, {})
+            cur[parts[-1]] = v
+        hp = trials[0]["hparams"] or {}
+        cfg["hyperparameters"] = {k: {"type": "const", "val": v} for k, v in hp.items()}
+        cfg["searcher"] = dict(cfg["searcher"], name="single", source_checkpoint_uuid=ck)
+        for k in ("max_trials", "max_concurrent_trials", "mode", "divisor", "max_rungs"):
+            cfg["searcher"].pop(k, None)
+        return self.create_experiment(cfg, row["model_def"], parent_id=eid)
 
     def _kill_allocation(self, a: Allocation) -> None:
         a.killed = True
@@ -624,6 +714,8 @@ class Master:
         self.sched.remove_request(a.id)
         a.state = "TERMINATED"
         self._on_allocation_exit(a)
+        if a.exp_id is not None and a.exp_id in self.experiments and self.experiments[a.exp_id].deferred:
+            self._drain_deferred(self.experiments[a.exp_id])
         self.cv.notify_all()
 
     def _on_allocation_exit(self, a: Allocation) -> None:
@@ -855,7 +947,13 @@ class Master:
                     continue
                 cutoff = now - int(days) * 86400
                 for t in self.db.all("SELECT id FROM trials WHERE experiment_id=? AND end_time IS NOT NULL AND "
-                                     "end_time < ?", [row["id"], cutoff]):
+                                     "end_time < ? AND log_retention_days IS NULL", [row["id"], cutoff]):
+                    cur = self.db.execute("DELETE FROM task_logs WHERE task_id=?", [f"trial-{t['id']}"])
+                    deleted += cur.rowcount or 0
+            # per-trial overrides (``det trial set log-retention``; -1 keeps forever)
+            for t in self.db.all("SELECT id, end_time, log_retention_days FROM trials WHERE "
+                                 "log_retention_days IS NOT NULL AND log_retention_days >= 0 AND end_time IS NOT NULL"):
+                if t["end_time"] < now - int(t["log_retention_days"]) * 86400:
                     cur = self.db.execute("DELETE FROM task_logs WHERE task_id=?", [f"trial-{t['id']}"])
                     deleted += cur.rowcount or 0
         return deleted

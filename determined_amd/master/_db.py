@@ -46,7 +46,8 @@ CREATE TABLE IF NOT EXISTS webhooks (
 CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
 """
 
-MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT")]
+MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT"),
+              ("models", "workspace", "TEXT DEFAULT 'Uncategorized'"), ("trials", "log_retention_days", "INTEGER")]
 
 JSON_COLS = {"config", "hparams", "metrics", "batch_metrics", "resources", "metadata", "searcher_snapshot", "labels",
              "searcher_state", "triggers", "proxy"}

@@ -20,6 +20,7 @@ from determined_amd.config import InvalidConfig
 from determined_amd.master._iam import AuthError, _public_user
 from determined_amd.master._iam_routes import add_iam_routes
 from determined_amd.master._ntsc import add_ntsc_routes
+from determined_amd.master._exp_routes import add_exp_routes
 from determined_amd.master._core import Master
 
 logger = logging.getLogger("determined_amd.master")
@@ -361,6 +362,7 @@ def build_routes(m: Master) -> List[Route]:
         return {}
 
     add_ntsc_routes(route, m)
+    add_exp_routes(route, m)
 
     @route("GET", "/api/v1/tasks")
     def list_tasks(q, b):
@@ -449,7 +451,10 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("PATCH", r"/api/v1/models/([^/]+)")
     def patch_model(q, b, name):
-        cols = {k: v for k, v in b.items() if k in ("description", "metadata", "labels", "notes", "archived")}
+        cols = {k: v for k, v in b.items() if k in ("description", "metadata", "labels", "notes", "archived",
+                                                    "workspace")}
+        if "workspace" in cols:
+            m.iam.workspace(cols["workspace"])  # must exist
         m.db.update("models", "name", urllib.parse.unquote(name), **cols)
         return {}
 
@@ -538,7 +543,8 @@ def build_routes(m: Master) -> List[Route]:
         row = m.db.one("SELECT * FROM templates WHERE name=?", [name])
         if row is None:
             raise HTTPError(404, f"template {name} not found")
-        return {"template": {"name": row["name"], "config": json.loads(row["config"])}}
+        cfg = row["config"]
+        return {"template": {"name": row["name"], "config": json.loads(cfg) if isinstance(cfg, str) else cfg}}
 
     @route("GET", "/metrics")
     def prom(q, b):
