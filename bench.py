@@ -65,11 +65,24 @@ def main() -> int:
                                 use_harness=not a.no_harness)
 
     t_w = time.perf_counter()
+    # the first warm-up step may spend minutes in MIOpen's solver search for shapes missing from
+    # the find-db: keep a heartbeat on stderr so supervisors do not mistake it for a hang
+    import threading
+
+    warm_done = threading.Event()
+
+    def heartbeat() -> None:
+        while not warm_done.wait(30.0):
+            print(f"[bench] warming up ({time.perf_counter() - t_w:.0f}s)", file=sys.stderr, flush=True)
+
+    if rank == 0:
+        threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(a.warmup):
         step_fn()
         if rank == 0:  # progress on stderr (stdout carries only the JSON line)
             torch.cuda.synchronize()
             print(f"[bench] warmup {i + 1}/{a.warmup} {time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
+    warm_done.set()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
