@@ -49,6 +49,12 @@ int damd_norm_bwd_blocks(int64_t);
 int damd_norm_bwd_launch(const void*, const void*, const float*, const float*, const void*, void*, float*,
                          float*, int64_t, int, int, int, int, hipStream_t);
 void damd_norm_wgrad_finalize_launch(const float*, const float*, int, int, void*, void*, int, hipStream_t);
+int damd_resid_norm_supported(int);
+void damd_resid_norm_fwd_launch(const void*, const void*, const void*, const void*, void*, void*, uint8_t*, float*,
+                                float*, int64_t, int, float, float, uint32_t, int, int, hipStream_t);
+int damd_resid_norm_bwd_launch(const void*, const void*, const void*, const float*, const float*, const void*,
+                               const uint8_t*, float, void*, void*, float*, float*, int64_t, int, int, int,
+                               hipStream_t);
 void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
@@ -59,6 +65,11 @@ void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, co
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
                         const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
                         hipStream_t, const uint8_t*);
+void damd_bn_pool_fwd_launch(const void*, void*, uint8_t*, int64_t, int, int, int, int, int, const void*, const void*,
+                             float*, float*, float, float, float*, float*, float*, float*, float*, int, int, hipStream_t);
+void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, int, int, int, int, int, const float*,
+                             const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
+                             hipStream_t);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
                                      int, int, float, int, hipStream_t);
@@ -390,6 +401,122 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// ---------------------------------------------------------------- residual add + dropout + LayerNorm
+bool resid_norm_supported(const at::Tensor& x) {
+  return x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
+         damd_resid_norm_supported(static_cast<int>(x.size(-1)));
+}
+
+// s = x + dropout(branch, p); y = LayerNorm(s).  Returns (s, y, mean, rstd, keep bits).
+std::vector<at::Tensor> resid_norm_fwd(const at::Tensor& x, const at::Tensor& branch, const at::Tensor& gamma,
+                                       const c10::optional<at::Tensor>& beta, double eps, double p, int64_t seed) {
+  TORCH_CHECK(resid_norm_supported(x), "resid_norm_fwd: unsupported input");
+  TORCH_CHECK(branch.sizes() == x.sizes() && branch.scalar_type() == x.scalar_type() && branch.is_contiguous(),
+              "resid_norm_fwd: branch must match x");
+  const int64_t H = x.size(-1), rows = x.numel() / H;
+  TORCH_CHECK(gamma.numel() == H, "gamma must have H elements");
+  auto fopts = x.options().dtype(at::kFloat);
+  auto sum = at::empty_like(x);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({rows}, fopts);
+  auto rstd = at::empty({rows}, fopts);
+  auto mask = at::empty({x.numel() / 8}, x.options().dtype(at::kByte));
+  const void* bp = beta.has_value() && beta->defined() ? beta->data_ptr() : nullptr;
+  damd_resid_norm_fwd_launch(x.data_ptr(), branch.data_ptr(), gamma.data_ptr(), bp, sum.data_ptr(), y.data_ptr(),
+                             mask.data_ptr<uint8_t>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                             static_cast<int>(H), static_cast<float>(eps), static_cast<float>(p),
+                             static_cast<uint32_t>(seed), dtype_code(x), dtype_code(gamma), cur_stream());
+  return {sum, y, mean, rstd, mask};
+}
+
+// Returns (d residual input, d branch, dgamma, dbeta).
+std::vector<at::Tensor> resid_norm_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& dres,
+                                       const at::Tensor& s, const at::Tensor& mean, const at::Tensor& rstd,
+                                       const at::Tensor& gamma, const at::Tensor& mask, double p, bool has_beta) {
+  TORCH_CHECK(dy.sizes() == s.sizes() && dy.is_contiguous() && dy.scalar_type() == s.scalar_type(), "bad dy");
+  const void* rp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    TORCH_CHECK(dres->sizes() == s.sizes() && dres->is_contiguous() && dres->scalar_type() == s.scalar_type(), "bad dres");
+    rp = dres->data_ptr();
+  }
+  const int64_t H = s.size(-1), rows = s.numel() / H;
+  TORCH_CHECK(mask.numel() == s.numel() / 8 && mask.scalar_type() == at::kByte, "bad keep-bit tensor");
+  auto fopts = s.options().dtype(at::kFloat);
+  auto dx = at::empty_like(s);
+  auto dbranch = at::empty_like(s);
+  const int cap = damd_norm_bwd_blocks(rows);
+  auto part_g = at::empty({cap, H}, fopts);
+  auto part_b = at::empty({cap, H}, fopts);  // the LayerNorm backward always writes both partial sets
+  const int W = damd_resid_norm_bwd_launch(dy.data_ptr(), rp, s.data_ptr(), mean.data_ptr<float>(),
+                                           rstd.data_ptr<float>(), gamma.data_ptr(), mask.data_ptr<uint8_t>(),
+                                           static_cast<float>(p), dx.data_ptr(), dbranch.data_ptr(),
+                                           part_g.data_ptr<float>(), part_b.data_ptr<float>(), rows,
+                                           static_cast<int>(H), dtype_code(s), dtype_code(gamma), cur_stream());
+  auto dgamma = at::empty({H}, gamma.options());
+  auto dbeta = has_beta ? at::empty({H}, gamma.options()) : at::empty({0}, gamma.options());
+  damd_norm_wgrad_finalize_launch(part_g.data_ptr<float>(), has_beta ? part_b.data_ptr<float>() : nullptr, W,
+                                  static_cast<int>(H), dgamma.data_ptr(), has_beta ? dbeta.data_ptr() : nullptr,
+                                  dtype_code(gamma), cur_stream());
+  return {dx, dbranch, dgamma, dbeta};
+}
+
+// ---------------------------------------------------------------- ResNet stem: BN + ReLU + MaxPool(3, 2, 1)
+// x: [N, C, H, W] channels-last (NHWC storage); returns (y [N, C, OH, OW] channels-last, argmax
+// uint8 [N*OH*OW*C], stats [4, C]).
+std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
+                                    const c10::optional<at::Tensor>& running_mean,
+                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps) {
+  TORCH_CHECK(x.dim() == 4 && bn_supported(x), "bn_pool_fwd: need a 4-d channels-last tensor with C % 8 == 0");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C, "weight/bias must have C elements");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    TORCH_CHECK(running_mean->scalar_type() == at::kFloat && running_var->scalar_type() == at::kFloat,
+                "running stats must be float32");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  auto fopts = x.options().dtype(at::kFloat);
+  const int nb = damd_bn_num_blocks(N * H * W, static_cast<int>(C));
+  auto part = at::empty({nb, 2, C}, fopts);
+  auto stats = at::empty({4, C}, fopts);
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N * OH * OW * C}, x.options().dtype(at::kByte));
+  damd_bn_pool_fwd_launch(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, static_cast<int>(H), static_cast<int>(W),
+                          static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW), weight.data_ptr(),
+                          bias.data_ptr(), rm, rv, static_cast<float>(momentum), static_cast<float>(eps),
+                          part.data_ptr<float>(), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
+                          stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), dtype_code(x), dtype_code(weight),
+                          cur_stream());
+  return {y, idx, stats};
+}
+
+std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& x,
+                                    const at::Tensor& stats, const at::Tensor& weight) {
+  TORCH_CHECK(x.dim() == 4 && bn_supported(x), "bn_pool_bwd: bad x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  TORCH_CHECK(dp.dim() == 4 && dp.size(0) == N && dp.size(1) == C && dp.size(2) == OH && dp.size(3) == OW &&
+              nhwc_dense(dp) && dp.scalar_type() == x.scalar_type(), "bn_pool_bwd: dp must be [N, C, OH, OW] channels-last");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == N * OH * OW * C && idx.is_contiguous(),
+              "bn_pool_bwd: bad argmax tensor");
+  auto fopts = x.options().dtype(at::kFloat);
+  const int nb = damd_bn_num_blocks(N * H * W, static_cast<int>(C));
+  auto part = at::empty({nb, 2, C}, fopts);
+  auto coef = at::empty({3, C}, fopts);
+  auto dgamma = at::empty({C}, weight.options());
+  auto dbeta = at::empty({C}, weight.options());
+  auto dx = at::empty_like(x);
+  damd_bn_pool_bwd_launch(dp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), N, static_cast<int>(H),
+                          static_cast<int>(W), static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW),
+                          stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
+                          stats[3].data_ptr<float>(), part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(),
+                          dbeta.data_ptr(), dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -527,6 +654,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("bn_apply", &bn_apply);
+  m.def("bn_pool_fwd", &bn_pool_fwd);
+  m.def("resid_norm_supported", &resid_norm_supported);
+  m.def("resid_norm_fwd", &resid_norm_fwd);
+  m.def("resid_norm_bwd", &resid_norm_bwd);
+  m.def("bn_pool_bwd", &bn_pool_bwd);
   m.doc() = "determined_amd CDNA4 HIP kernels";
   m.def("build_chunk_table", &build_chunk_table);
   m.def("chunk_entry_bytes", &chunk_entry_bytes);

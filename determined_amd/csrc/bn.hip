@@ -19,6 +19,8 @@
 
 #include "common.h"
 
+#include <math.h>
+
 namespace damd {
 
 constexpr int kBNThreads = 256;
@@ -119,16 +121,18 @@ bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int64_t rows_per_bloc
 }
 
 // ----------------------------------------------------------------------------- partial reduction
-// Sums part[nb][2][C] over nb for 64 channels per block.  1024 threads = 64 channels x 16
+// Sums part[nb][2][C] over nb for 16 channels per block.  1024 threads = 16 channels x 64
 // lanes; each lane keeps 8 independent accumulators so its loads are issued back to back
 // (a serial per-thread chain over ~1000 partial rows costs ~70 us in L2 round trips).
 // Result (deterministic order) lands in thread lane==0's (s, ss).
 constexpr int kFinThreads = 1024;
-constexpr int kFinLanes = kFinThreads / 64;
+constexpr int kFinCh = 16;                         // channels per block
+constexpr int kFinLanes = kFinThreads / kFinCh;    // 64 row-lanes per channel: ~2 load rounds for nb=1024
+// (finalize kernels are pure latency: 64 lanes x 8 accumulators keep the dependent rounds short)
 
 __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int nb, int C, int c, int q,
                                                 float& s, float& ss) {
-  __shared__ float rs[kFinLanes][64], rq[kFinLanes][64];
+  __shared__ float rs[kFinLanes][kFinCh], rq[kFinLanes][kFinCh];
   float a0[8], a1[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) { a0[u] = 0.f; a1[u] = 0.f; }
@@ -150,7 +154,7 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
   float t0 = 0.f, t1 = 0.f;
 #pragma unroll
   for (int u = 0; u < 8; ++u) { t0 += a0[u]; t1 += a1[u]; }
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x % kFinCh;
   rs[q][lane] = t0;
   rq[q][lane] = t1;
   __syncthreads();
@@ -164,7 +168,7 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
 
 // ----------------------------------------------------------------------------- fwd finalize
 // Produces mean/invstd (saved for bwd), folded scale/shift (for apply) and updates the
-// running statistics.  grid = ceil(C/64) blocks of 1024 threads.
+// running statistics.  grid = ceil(C/16) blocks of 1024 threads.
 template <typename WT>
 __global__ void __launch_bounds__(kFinThreads)
 bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, int64_t rows_per_block,
@@ -172,8 +176,8 @@ bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, int
                    const WT* __restrict__ w, const WT* __restrict__ b, float* __restrict__ run_mean,
                    float* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ invstd_out,
                    float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x % kFinCh, q = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + lane;
   float s, ss;
   reduce_partials(part, nb, C, c, q, s, ss);
   if (q == 0 && c < C) {
@@ -333,8 +337,8 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
                        const float* __restrict__ mean, const float* __restrict__ invstd,
                        const float* __restrict__ scale, WT* __restrict__ dgamma, WT* __restrict__ dbeta,
                        float* __restrict__ coef /* [3][C] */) {
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x % kFinCh, q = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + lane;
   float s, sx;
   reduce_partials(part, nb, C, c, q, s, sx);
   if (q == 0 && c < C) {
@@ -392,6 +396,176 @@ bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* 
   }
 }
 
+
+// ============================================================================= stem: BN+ReLU+MaxPool
+// ResNet stem: y = maxpool3x3/s2/p1(relu(bn(x))).  Instead of writing relu(bn(x)) (N*H*W*C) and
+// reading it back in a separate pooling pass, one kernel applies BN+ReLU on the fly while it
+// pools and stores the pooled output plus the argmax (0..8, row-major in the window, first max
+// wins as in PyTorch) as one byte per element.  The backward never materialises the full-size
+// pooled gradient either: both BN-backward passes gather it from (dp, argmax) of the <= 4
+// windows that contain each input pixel.  Traffic (bf16, C=64, 112->56): fwd reads x once and
+// writes 1/4 + 1/8 of it; bwd reads x and the small (dp, argmax) twice and writes dx once.
+struct PoolGeo {
+  int H, W, OH, OW;
+};
+
+// window index of input (h, w) inside output window (oh, ow) (kernel 3, stride 2, pad 1)
+__device__ __forceinline__ int win_pos(int h, int w, int oh, int ow) { return (h - 2 * oh + 1) * 3 + (w - 2 * ow + 1); }
+
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+                           T* __restrict__ y, uint8_t* __restrict__ idx, int64_t Vout, int TPR, PoolGeo g) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
+  const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
+  const int cg = static_cast<int>(T0 % TPR);  // stride is a multiple of TPR
+  const int C = TPR * 8;
+  float sc[8], sh[8];
+  V8<float>::ld(scale + cg * 8, sc);
+  V8<float>::ld(shift + cg * 8, sh);
+  for (int64_t v = T0; v < Vout; v += stride) {
+    const int64_t pix = v / TPR;  // (n, oh, ow)
+    const int ow = static_cast<int>(pix % g.OW);
+    const int oh = static_cast<int>((pix / g.OW) % g.OH);
+    const int64_t n = pix / (static_cast<int64_t>(g.OW) * g.OH);
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = 2 * oh - 1 + kh;
+      if (h < 0 || h >= g.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = 2 * ow - 1 + kw;
+        if (w < 0 || w >= g.W) continue;
+        float a[8];
+        V8<T>::ld(x + ((n * g.H + h) * g.W + w) * C + cg * 8, a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float r = fmaxf(a[k] * sc[k] + sh[k], 0.f);
+          if (r > best[k]) { best[k] = r; arg[k] = kh * 3 + kw; }
+        }
+      }
+    }
+    V8<T>::st(y + v * 8, best);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { lo |= static_cast<uint32_t>(arg[k]) << (8 * k); hi |= static_cast<uint32_t>(arg[k + 4]) << (8 * k); }
+    *reinterpret_cast<uint2*>(idx + v * 8) = make_uint2(lo, hi);
+  }
+}
+
+// d(relu output) at input (n, h, w), channels cg*8..+8, gathered from the pooled gradient
+template <typename T>
+__device__ __forceinline__ void pool_grad_gather(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int64_t n,
+                                                 int h, int w, int cg, int C, const PoolGeo& g, float* dr) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dr[k] = 0.f;
+  const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, g.OH - 1);
+  const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, g.OW - 1);
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int64_t o = ((n * g.OH + oh) * g.OW + ow) * C + cg * 8;
+      const uint2 ii = *reinterpret_cast<const uint2*>(idx + o);
+      const int pos = win_pos(h, w, oh, ow);
+      float d[8];
+      V8<T>::ld(dp + o, d);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (static_cast<int>((ii.x >> (8 * k)) & 0xFFu) == pos) dr[k] += d[k];
+        if (static_cast<int>((ii.y >> (8 * k)) & 0xFFu) == pos) dr[k + 4] += d[k + 4];
+      }
+    }
+  }
+}
+
+// BN-backward reduce over dz = maxpool_bwd(dp) * [bn(x) > 0]: part[nb][2][C] = (sum dz, sum dz*(x-mean))
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
+                             const float* __restrict__ mean, const float* __restrict__ scale,
+                             const float* __restrict__ shift, int64_t M, int C, int64_t rows_per_block,
+                             float* __restrict__ part, PoolGeo g) {
+  const Geo geo_ = geo(C);
+  const int tid = threadIdx.x;
+  const int cg0 = geo_.TPR <= kBNThreads ? tid % geo_.TPR : tid;
+  const int rsub = geo_.TPR <= kBNThreads ? tid / geo_.TPR : 0;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  __shared__ float red[kBNThreads * 8];
+  for (int gi = 0; gi < geo_.G; ++gi) {
+    const int cg = cg0 + gi * kBNThreads;
+    float mu[8], sc[8], sh[8], s[8], sx[8];
+    V8<float>::ld(mean + cg * 8, mu);
+    V8<float>::ld(scale + cg * 8, sc);
+    V8<float>::ld(shift + cg * 8, sh);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; sx[k] = 0.f; }
+    for (int64_t r = r0 + rsub; r < r1; r += geo_.RS) {
+      const int w = static_cast<int>(r % g.W);
+      const int h = static_cast<int>((r / g.W) % g.H);
+      const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
+      float a[8], dr[8];
+      V8<T>::ld(x + r * C + cg * 8, a);
+      pool_grad_gather(dp, idx, n, h, w, cg, C, g, dr);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[k] : 0.f;
+        s[k] += dz;
+        sx[k] += dz * (a[k] - mu[k]);
+      }
+    }
+    for (int which = 0; which < 2; ++which) {
+      float* v = which == 0 ? s : sx;
+      if (geo_.RS > 1) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[tid * 8 + k] = v[k];
+        __syncthreads();
+        if (rsub == 0) {
+          for (int q = 1; q < geo_.RS; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += red[(q * geo_.TPR + cg0) * 8 + k];
+        }
+      }
+      if (rsub == 0) V8<float>::st(part + (static_cast<int64_t>(blockIdx.x) * 2 + which) * C + cg * 8, v);
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
+                            const float* __restrict__ scale, const float* __restrict__ shift,
+                            const float* __restrict__ coef, int C, T* __restrict__ dx, int64_t V, int TPR, PoolGeo g) {
+  const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
+  const int cg = static_cast<int>(T0 % TPR);
+  float A[8], B[8], Cc[8], sc[8], sh[8];
+  V8<float>::ld(coef + cg * 8, A);
+  V8<float>::ld(coef + C + cg * 8, B);
+  V8<float>::ld(coef + 2 * C + cg * 8, Cc);
+  V8<float>::ld(scale + cg * 8, sc);
+  V8<float>::ld(shift + cg * 8, sh);
+  for (int64_t v = T0; v < V; v += stride) {
+    const int64_t r = v / TPR;
+    const int w = static_cast<int>(r % g.W);
+    const int h = static_cast<int>((r / g.W) % g.H);
+    const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
+    float a[8], dr[8], o[8];
+    V8<T>::ld(x + v * 8, a);
+    pool_grad_gather(dp, idx, n, h, w, cg, C, g, dr);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[k] : 0.f;
+      o[k] = A[k] * dz + B[k] * a[k] + Cc[k];
+    }
+    V8<T>::st(dx + v * 8, o);
+  }
+}
+
 }  // namespace damd
 
 using namespace damd;
@@ -435,7 +609,7 @@ void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int 
     hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
   else
     hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
-  const dim3 fg((C + 63) / 64);
+  const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
     hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
                        static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
@@ -502,10 +676,10 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   }
 #undef RED
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + 63) / 64), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
@@ -529,5 +703,71 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   }
 #undef BAP
 #undef BAPM
+  DAMD_CHECK_LAUNCH();
+}
+
+
+// ----------------------------------------------------------------------------- stem launchers
+// x: [N, H, W, C] (NHWC); y / idx: [N, OH, OW, C]; 3x3 / stride 2 / pad 1 pooling.
+void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, int H, int W, int C, int OH, int OW,
+                             const void* w, const void* b, float* run_mean, float* run_var, float momentum, float eps,
+                             float* part, float* mean, float* invstd, float* scale, float* shift, int x_dtype,
+                             int w_dtype, hipStream_t st) {
+  const int64_t M = N * H * W;
+  int nb;
+  const int64_t rpb = rows_per_block_for(M, C, &nb);
+  if (x_dtype == 1)
+    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+  const dim3 fg((C + kFinCh - 1) / kFinCh);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+                       static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+                       static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
+  const int TPR = C / 8;
+  const int64_t Vout = N * OH * OW * TPR;
+  const PoolGeo g{H, W, OH, OW};
+  const dim3 ag(apply_grid(Vout, TPR));
+  if (x_dtype == 1)
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift,
+                       static_cast<bf16_t*>(y), idx, Vout, TPR, g);
+  else
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift,
+                       static_cast<float*>(y), idx, Vout, TPR, g);
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, int64_t N, int H, int W, int C, int OH,
+                             int OW, const float* mean, const float* invstd, const float* scale, const float* shift,
+                             float* part, float* coef, void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype,
+                             hipStream_t st) {
+  const int64_t M = N * H * W;
+  int nb;
+  const int64_t rpb = rows_per_block_for(M, C, &nb);
+  const PoolGeo g{H, W, OH, OW};
+  if (x_dtype == 1)
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
+                       static_cast<const bf16_t*>(x), mean, scale, shift, M, C, rpb, part, g);
+  else
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
+                       static_cast<const float*>(x), mean, scale, shift, M, C, rpb, part, g);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
+  const int TPR = C / 8;
+  const int64_t V = M * TPR;
+  const dim3 ag(apply_grid(V, TPR));
+  if (x_dtype == 1)
+    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
+                       static_cast<const bf16_t*>(x), scale, shift, coef, C, static_cast<bf16_t*>(dx), V, TPR, g);
+  else
+    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
+                       static_cast<const float*>(x), scale, shift, coef, C, static_cast<float*>(dx), V, TPR, g);
   DAMD_CHECK_LAUNCH();
 }

@@ -44,11 +44,33 @@ template <> struct Vec8<float> {
 };
 
 // ------------------------------------------------------------------ forward (register-resident)
-template <typename T, typename WT, int NV, bool RMS>
+// Residual fusion (RESID): the normalised row is s = x + dropout(branch) (the transformer's
+// residual add), s is written out (it is the next residual) together with one keep-bit per
+// element, and the LayerNorm runs on s from registers: one pass instead of dropout + add + LN.
+struct ResidArgs {
+  const void* branch;   // [rows, H]
+  void* sum_out;        // [rows, H]
+  uint8_t* mask;        // [rows * H / 8] keep bits
+  float keep_scale;     // 1 / (1 - p)
+  uint32_t seed;
+  uint32_t drop_thresh; // element dropped iff hash < drop_thresh (p * 2^32); 0 = no dropout
+};
+
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint64_t e) {
+  uint32_t h = static_cast<uint32_t>(e) ^ (static_cast<uint32_t>(e >> 32) * 0x85EBCA6Bu) ^ (seed * 0x9E3779B9u);
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+
+template <typename T, typename WT, int NV, bool RMS, bool RESID = false>
 __global__ void __launch_bounds__(kNormThreads)
 norm_fwd_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, const WT* __restrict__ beta,
                 T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                int64_t rows, int H, float eps) {
+                int64_t rows, int H, float eps, ResidArgs ra = ResidArgs{}) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
   if (row >= rows) return;
@@ -60,6 +82,25 @@ norm_fwd_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, const WT*
     const int c = (j * kWave + lane) * kVecElems;
     if (c < H) {
       Vec8<T>::ld(xr + c, v[j]);
+      if (RESID) {
+        float bv[kVecElems];
+        Vec8<T>::ld(static_cast<const T*>(ra.branch) + row * H + c, bv);
+        uint32_t bits = 0;
+        const uint64_t e0 = static_cast<uint64_t>(row) * H + c;
+#pragma unroll
+        for (int k = 0; k < kVecElems; ++k) {
+          const bool keep = ra.drop_thresh == 0u || drop_hash(ra.seed, e0 + k) >= ra.drop_thresh;
+          bits |= (keep ? 1u : 0u) << k;
+          v[j][k] += keep ? bv[k] * ra.keep_scale : 0.f;
+        }
+        Vec8<T>::st(static_cast<T*>(ra.sum_out) + row * H + c, v[j]);
+        // normalise the value as stored (rounded to T) so forward and backward agree exactly
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int k = 0; k < kVecElems; ++k) v[j][k] = bf2f(f2bf(v[j][k]));
+        }
+        ra.mask[e0 >> 3] = static_cast<uint8_t>(bits);
+      }
 #pragma unroll
       for (int k = 0; k < kVecElems; ++k) s += v[j][k];
     } else {
@@ -135,11 +176,22 @@ norm_fwd_generic_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, c
 // Weight gradients: the 4 waves' column partials are reduced in LDS and each block writes one
 // fp32 partial row (part_g / part_b: [gridDim.x, H]); wgrad_finalize_kernel sums the rows and
 // writes dgamma / dbeta in the weight dtype.
-template <typename T, typename WT, int NV, bool RMS>
+// RESID backward: x is the saved sum s; the residual's own gradient (dres_in, from the next
+// use of s) is added to the LN input-gradient, written as the residual gradient dx, and the
+// branch gradient is dx * keep / (1 - p) from the saved bits.
+struct ResidBwdArgs {
+  const void* dres_in;  // [rows, H] (may be null: no external gradient)
+  void* dbranch;        // [rows, H]
+  const uint8_t* mask;
+  float keep_scale;
+};
+
+template <typename T, typename WT, int NV, bool RMS, bool RESID = false>
 __global__ void __launch_bounds__(kNormThreads)
 norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* __restrict__ mean_in,
                 const float* __restrict__ rstd_in, const WT* __restrict__ gamma, T* __restrict__ dx,
-                float* __restrict__ part_g, float* __restrict__ part_b, int64_t rows, int H) {
+                float* __restrict__ part_g, float* __restrict__ part_b, int64_t rows, int H,
+                ResidBwdArgs rb = ResidBwdArgs{}) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave_id = static_cast<int64_t>(blockIdx.x) * (kNormThreads / kWave) + threadIdx.x / kWave;
   const int64_t n_waves = static_cast<int64_t>(gridDim.x) * (kNormThreads / kWave);
@@ -188,6 +240,19 @@ norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x, const float* 
 #pragma unroll
         for (int k = 0; k < kVecElems; ++k)
           o[k] = rstd * (g[j][k] * gw[j][k] - xh[j][k] * c1 - c2);
+        if (RESID) {
+          if (rb.dres_in != nullptr) {
+            float r[kVecElems];
+            Vec8<T>::ld(static_cast<const T*>(rb.dres_in) + row * H + c, r);
+#pragma unroll
+            for (int k = 0; k < kVecElems; ++k) o[k] += r[k];
+          }
+          const uint32_t bits = rb.mask[(static_cast<uint64_t>(row) * H + c) >> 3];
+          float db[kVecElems];
+#pragma unroll
+          for (int k = 0; k < kVecElems; ++k) db[k] = (bits >> k) & 1u ? o[k] * rb.keep_scale : 0.f;
+          Vec8<T>::st(static_cast<T*>(rb.dbranch) + row * H + c, db);
+        }
         Vec8<T>::st(dx + row * H + c, o);
       }
     }
@@ -383,6 +448,65 @@ void damd_norm_fwd_launch(const void* x, const void* gamma, const void* beta, vo
   else if (w_dtype == 1) FD(float, bf16_t);
   else FD(float, float);
 #undef FD
+}
+
+int damd_norm_bwd_blocks(int64_t rows);
+
+// Residual-fused LayerNorm (register-resident path only: H % 8 == 0 and H <= 64*8*16 forward,
+// <= 64*8*4 backward; the host checks damd_resid_norm_supported first).
+int damd_resid_norm_supported(int H) {
+  const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
+  return (H % kVecElems) == 0 && nv <= 4;
+}
+
+void damd_resid_norm_fwd_launch(const void* x, const void* branch, const void* gamma, const void* beta, void* sum_out,
+                                void* y, uint8_t* mask, float* mean, float* rstd, int64_t rows, int H, float eps,
+                                float p, uint32_t seed, int x_dtype, int w_dtype, hipStream_t st) {
+  ResidArgs ra;
+  ra.branch = branch;
+  ra.sum_out = sum_out;
+  ra.mask = mask;
+  ra.keep_scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  ra.seed = seed;
+  ra.drop_thresh = p > 0.f ? static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0) : 0u;
+  const dim3 grid(static_cast<unsigned>((rows + 3) / 4)), block(kNormThreads);
+  const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
+#define RF(T, WT, N) hipLaunchKernelGGL((norm_fwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(x), \
+    static_cast<const WT*>(gamma), static_cast<const WT*>(beta), static_cast<T*>(y), mean, rstd, rows, H, eps, ra)
+#define RFN(T, WT) do { switch (nv) { case 1: RF(T, WT, 1); break; case 2: RF(T, WT, 2); break; default: RF(T, WT, 4); } } while (0)
+  if (x_dtype == 1 && w_dtype == 1) RFN(bf16_t, bf16_t);
+  else if (x_dtype == 1) RFN(bf16_t, float);
+  else if (w_dtype == 1) RFN(float, bf16_t);
+  else RFN(float, float);
+#undef RFN
+#undef RF
+  DAMD_CHECK_LAUNCH();
+}
+
+// Returns the number of partial rows (input of damd_norm_wgrad_finalize_launch).
+int damd_resid_norm_bwd_launch(const void* dy, const void* dres_in, const void* s, const float* mean, const float* rstd,
+                               const void* gamma, const uint8_t* mask, float p, void* dx, void* dbranch,
+                               float* part_g, float* part_b, int64_t rows, int H, int x_dtype, int w_dtype,
+                               hipStream_t st) {
+  ResidBwdArgs rb;
+  rb.dres_in = dres_in;
+  rb.dbranch = dbranch;
+  rb.mask = mask;
+  rb.keep_scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const int nb = damd_norm_bwd_blocks(rows);
+  const dim3 grid(nb), block(kNormThreads);
+  const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
+#define RB(T, WT, N) hipLaunchKernelGGL((norm_bwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(dy), \
+    static_cast<const T*>(s), mean, rstd, static_cast<const WT*>(gamma), static_cast<T*>(dx), part_g, part_b, rows, H, rb)
+#define RBN(T, WT) do { switch (nv) { case 1: RB(T, WT, 1); break; case 2: RB(T, WT, 2); break; default: RB(T, WT, 4); } } while (0)
+  if (x_dtype == 1 && w_dtype == 1) RBN(bf16_t, bf16_t);
+  else if (x_dtype == 1) RBN(bf16_t, float);
+  else if (w_dtype == 1) RBN(float, bf16_t);
+  else RBN(float, float);
+#undef RBN
+#undef RB
+  DAMD_CHECK_LAUNCH();
+  return nb;
 }
 
 // Number of blocks used by the backward grid (=> partial rows = 4 * blocks).

@@ -7,7 +7,8 @@ self-contained implementation of the GPT-2 architecture (pre-LN blocks, learned 
 tied input/output embedding, GELU-tanh MLP) laid out for MI355X:
 
 * bf16 weights and activations; LayerNorms are the wave-per-row fused HIP kernels
-  (``ops.FusedLayerNorm``, ``csrc/norm.hip``);
+  (``ops.FusedLayerNorm``, ``csrc/norm.hip``), each fused with the residual add + dropout
+  that precedes it (one kernel instead of dropout, add and LayerNorm);
 * QKV / output / MLP projections are plain ``[B*T, d] x [d, n]`` GEMMs (hipBLASLt, MFMA);
 * attention is the hand-written MFMA flash-attention kernel (``ops.attention.qkv_attention``,
   ``csrc/attention.hip``) on the packed QKV projection: no [T, T] score matrix in HBM and a
@@ -68,14 +69,15 @@ class CausalSelfAttention(nn.Module):
         self.attn_dropout = cfg.attn_dropout
         self.resid_drop = nn.Dropout(cfg.dropout)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual_dropout: bool = True) -> torch.Tensor:
         B, T, C = x.shape
         qkv = self.c_attn(x).view(B, T, 3, self.n_head, C // self.n_head)
         # fused MFMA flash attention on the packed projection; returns [B, H, T, D] laid out
         # as [B, T, H, D], so merging the heads below is a view
         y = qkv_attention(qkv, causal=True, dropout_p=self.attn_dropout if self.training else 0.0)
         y = y.transpose(1, 2).reshape(B, T, C)
-        return self.resid_drop(self.c_proj(y))
+        out = self.c_proj(y)
+        return self.resid_drop(out) if residual_dropout else out
 
 
 class MLP(nn.Module):
@@ -85,8 +87,9 @@ class MLP(nn.Module):
         self.c_proj = FusedLinear(4 * cfg.n_embd, cfg.n_embd)
         self.drop = nn.Dropout(cfg.dropout)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+    def forward(self, x: torch.Tensor, residual_dropout: bool = True) -> torch.Tensor:
+        out = self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+        return self.drop(out) if residual_dropout else out
 
 
 class Block(nn.Module):
@@ -100,6 +103,14 @@ class Block(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x + self.attn(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
+
+    def forward_fused(self, x: torch.Tensor, h1: torch.Tensor, p: float):
+        """Given the residual stream ``x`` and ``h1 = ln_1(x)``: returns ``(x', m)`` where
+        ``x' = x + dropout(attn(h1))`` (fused with ``ln_2``) and ``m`` is the MLP branch whose
+        residual add + dropout the caller fuses into the next LayerNorm."""
+        a = self.attn(h1, residual_dropout=False)
+        x, h2 = self.ln_2(x, branch=a, p=p)
+        return x, self.mlp(h2, residual_dropout=False)
 
 
 class GPT2LMHeadModel(nn.Module):
@@ -140,12 +151,23 @@ class GPT2LMHeadModel(nn.Module):
         B, T = input_ids.shape
         pos = torch.arange(T, device=input_ids.device)
         x = self.drop(self.wte(input_ids) + self.wpe(pos))
-        for blk in self.h:
-            if self.config.activation_checkpointing and self.training:
-                x = checkpoint(blk, x, use_reentrant=False)
+        ckpt = self.config.activation_checkpointing and self.training
+        if not x.is_cuda:
+            for blk in self.h:
+                x = checkpoint(blk, x, use_reentrant=False) if ckpt else blk(x)
+            return self.ln_f(x)
+        # every residual add + dropout is fused into the following LayerNorm kernel
+        # (ln_2 of the same block, ln_1 of the next, ln_f after the last)
+        p = self.config.dropout if self.training else 0.0
+        h = self.h[0].ln_1(x)
+        for i, blk in enumerate(self.h):
+            if ckpt:
+                x, m = checkpoint(blk.forward_fused, x, h, p, use_reentrant=False)
             else:
-                x = blk(x)
-        return self.ln_f(x)
+                x, m = blk.forward_fused(x, h, p)
+            nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
+            x, h = nxt(x, branch=m, p=p)
+        return h
 
     def forward(self, input_ids: torch.Tensor, labels: Optional[torch.Tensor] = None) -> Any:
         """Returns logits ``[B, T, vocab]`` or, with ``labels``, the mean next-token loss."""

@@ -101,7 +101,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        # stem BN + ReLU + max-pool in one fused kernel pair (ops/bn.py: forward_maxpool)
+        x = self.bn1.forward_maxpool(self.conv1(x), self.maxpool)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

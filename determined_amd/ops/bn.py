@@ -43,6 +43,30 @@ class _BNActFn(torch.autograd.Function):
                 dres if ctx.has_res else None, None, None, None)
 
 
+class _BNReLUPoolFn(torch.autograd.Function):
+    """``maxpool3x3s2p1(relu(bn(x)))`` for the ResNet stem (csrc/bn.hip ``bn_relu_maxpool``):
+    the full-size activation is never written and the pooling backward is gathered inside the
+    two BN-backward passes."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        from determined_amd import ops
+
+        y, idx, stats = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum), float(eps))
+        ctx.save_for_backward(x, idx, stats, weight)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from determined_amd import ops
+
+        x, idx, stats, weight = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight)
+        return dx, dg, db, None, None, None, None
+
+
 def _torch_bn_act(bn: nn.BatchNorm2d, x, residual, relu, momentum):
     if bn.running_mean is not None and bn.running_mean.dtype != x.dtype:
         # low-precision activations with fp32 statistics: normalise in fp32
@@ -111,6 +135,26 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 y = y + residual
             return F.relu(y) if self.act else y
         return e.bn_apply(x, scale, shift, residual, self.act)
+
+    def forward_maxpool(self, x: torch.Tensor, pool: nn.MaxPool2d) -> torch.Tensor:
+        """``pool(self(x))`` with the fused stem kernels when ``pool`` is the ResNet 3x3/s2/p1
+        max-pool, training mode and a supported channels-last GPU tensor; exact composition
+        otherwise."""
+        fusable = (self.act and self.affine and x.is_cuda and x.dim() == 4 and self.training and
+                   self.track_running_stats and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and
+                   pool.padding in (1, (1, 1)) and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and
+                   not pool.return_indices)
+        if fusable:
+            from determined_amd import ops
+
+            fusable = ops.ext().bn_supported(x) and x.is_contiguous(memory_format=torch.channels_last)
+        if not fusable:
+            return pool(self(x))
+        momentum = 0.0 if self.momentum is None else self.momentum
+        self._nbt_host = self._nbt() + 1
+        if self.momentum is None:
+            momentum = 1.0 / float(self._nbt_host)
+        return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, momentum, self.eps)
 
     def _apply(self, fn, recurse: bool = True):
         # Running statistics always stay fp32 (a bf16 running_var loses the update signal).

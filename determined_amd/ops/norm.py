@@ -46,6 +46,52 @@ class _NormFn(torch.autograd.Function):
         return dx, dg, db, None, None
 
 
+class _ResidNormFn(torch.autograd.Function):
+    """``s = x + dropout(branch, p)``, ``y = LayerNorm(s)`` in one row-per-wave kernel
+    (csrc/norm.hip RESID path); returns (s, y).  Backward: one kernel that adds the gradient
+    arriving at ``s`` from its later use to the LayerNorm input-gradient and emits the branch
+    gradient through the saved keep bits."""
+
+    @staticmethod
+    def forward(ctx, x, branch, weight, bias, eps, p, seed):
+        from determined_amd import ops
+
+        s, y, mean, rstd, mask = ops.ext().resid_norm_fwd(x.contiguous(), branch.contiguous(), weight.contiguous(),
+                                                          bias, float(eps), float(p), int(seed))
+        ctx.save_for_backward(s, weight, mean, rstd, mask)
+        ctx.p = float(p)
+        ctx.has_bias = bias is not None
+        ctx.mark_non_differentiable(mask)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        from determined_amd import ops
+
+        s, weight, mean, rstd, mask = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dx, dbranch, dg, db = ops.ext().resid_norm_bwd(dy.contiguous(), None if ds is None else ds.contiguous(), s,
+                                                       mean, rstd, weight.contiguous(), mask, ctx.p, ctx.has_bias)
+        return dx, dbranch, dg.to(weight.dtype), (db.to(weight.dtype) if ctx.has_bias else None), None, None, None
+
+
+def residual_dropout_layer_norm(x: torch.Tensor, branch: torch.Tensor, norm: "FusedLayerNorm", p: float = 0.0,
+                                training: bool = True):
+    """``s = x + dropout(branch, p)``; returns ``(s, norm(s))``.  Fused on supported GPU tensors
+    (H % 8 == 0, H <= 2048), exact PyTorch composition otherwise."""
+    p = float(p) if training else 0.0
+    if x.is_cuda:
+        from determined_amd import ops
+
+        e = ops.ext()
+        if e.resid_norm_supported(x) and branch.dtype == x.dtype and branch.shape == x.shape:
+            seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if p > 0 else 0
+            return _ResidNormFn.apply(x, branch, norm.weight, norm.bias, norm.eps, p, seed)
+    s = x + torch.nn.functional.dropout(branch, p, training=p > 0)
+    return s, norm(s)
+
+
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5):
     if not x.is_cuda:
         return _ref_norm(x, weight, bias, eps, False)
@@ -76,7 +122,11 @@ class FusedLayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(self.normalized_shape, **fk), requires_grad=elementwise_affine) \
             if bias else None
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, branch: Optional[torch.Tensor] = None, p: float = 0.0):
+        """``norm(x)``, or with ``branch``: ``(s, norm(s))`` for ``s = x + dropout(branch, p)``
+        (residual add + dropout fused into the LayerNorm kernel)."""
+        if branch is not None:
+            return residual_dropout_layer_norm(x, branch, self, p, self.training)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
     def extra_repr(self) -> str:

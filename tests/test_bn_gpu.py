@@ -95,3 +95,38 @@ def test_bn_eval_matches(bnmod):
 def test_bf16_model_keeps_fp32_running_stats(bnmod):
     m = bnmod.BatchNormAct2d(64).cuda().to(torch.bfloat16)
     assert m.running_mean.dtype == torch.float32 and m.weight.dtype == torch.bfloat16
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 13, 10), (2, 8, 7, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_relu_maxpool_fused_matches_reference(bnmod, shape, dtype):
+    """ResNet stem: fused BN+ReLU+MaxPool(3,2,1) fwd/bwd vs the fp32 PyTorch composition."""
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    m = bnmod.BatchNormAct2d(C).cuda()
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(N, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = m.forward_maxpool(x, pool)
+    ref_bn = torch.nn.BatchNorm2d(C).cuda()
+    ref_bn.load_state_dict({k: v for k, v in m.state_dict().items()}, strict=False)
+    with torch.no_grad():
+        ref_bn.weight.copy_(m.weight.float())
+        ref_bn.bias.copy_(m.bias.float())
+        ref_bn.running_mean.zero_()
+        ref_bn.running_var.fill_(1.0)
+    xr = x.detach().float().requires_grad_(True)
+    yr = pool(torch.relu(ref_bn(xr)))
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == yr.shape
+    g = torch.randn_like(yr).to(dtype)  # both sides get the same (dtype-rounded) upstream gradient
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    torch.testing.assert_close(m.weight.grad.float(), ref_bn.weight.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(m.bias.grad.float(), ref_bn.bias.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(m.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-3)

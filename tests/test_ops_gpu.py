@@ -196,3 +196,44 @@ def test_ddp_single_rank_grads_match(ops):
         m_ref(x).sum().backward()
         for (n, p), (_, q) in zip(m.named_parameters(), m_ref.named_parameters()):
             torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-4, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [64, 1024, 1600])
+def test_residual_dropout_layernorm_fused(dtype, H):
+    """s = x + dropout(b); y = LN(s): fused kernel vs fp32 PyTorch (p=0 exact path; p>0 checks
+    the keep-mask statistics and that fwd/bwd use the same mask)."""
+    from determined_amd.ops.norm import FusedLayerNorm
+
+    torch.manual_seed(0)
+    ln = FusedLayerNorm(H).cuda().to(dtype)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(3, 37, H, device="cuda", dtype=dtype, requires_grad=True)
+    b = torch.randn(3, 37, H, device="cuda", dtype=dtype, requires_grad=True)
+    s, y = ln(x, branch=b, p=0.0)
+    xr, br = x.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    sr = xr + br
+    yr = torch.nn.functional.layer_norm(sr, (H,), ln.weight.float(), ln.bias.float(), ln.eps)
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(s.float(), sr, **tol)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    gs, gy = torch.randn_like(sr), torch.randn_like(yr)
+    torch.autograd.backward([s, y], [gs.to(dtype), gy.to(dtype)])
+    torch.autograd.backward([sr, yr], [gs, gy])
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    torch.testing.assert_close(b.grad.float(), br.grad, **tol)
+    # dropout: about p of the branch is dropped, kept elements scaled by 1/(1-p), and the
+    # branch gradient flows exactly through the kept elements
+    p = 0.25
+    x2 = torch.zeros(64, H, device="cuda", dtype=dtype)
+    b2 = torch.ones(64, H, device="cuda", dtype=dtype, requires_grad=True)
+    ln.train()
+    s2, y2 = ln(x2, branch=b2, p=p)
+    kept = s2.float() != 0
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.02
+    torch.testing.assert_close(s2.float()[kept], torch.full_like(s2.float()[kept], 1 / (1 - p)), rtol=1e-2, atol=1e-2)
+    s2.backward(torch.ones_like(s2))
+    torch.testing.assert_close(b2.grad.float(), kept.float() / (1 - p), rtol=1e-2, atol=1e-2)
