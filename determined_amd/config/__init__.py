@@ -135,11 +135,16 @@ HP_TYPES = ("const", "int", "double", "log", "categorical")
 CHECKPOINT_POLICIES = ("best", "all", "none")
 
 
+_LENGTH_UNITS = {"batches", "records", "epochs"}
+
+
 def _merge_defaults(cfg: Dict[str, Any], defaults: Dict[str, Any]) -> Dict[str, Any]:
     for k, dv in defaults.items():
         if k not in cfg or cfg[k] is None and dv is not None and isinstance(dv, dict):
             cfg[k] = copy.deepcopy(dv)
         elif isinstance(dv, dict) and isinstance(cfg.get(k), dict) and dv:
+            if set(dv) <= _LENGTH_UNITS and set(cfg[k]) & _LENGTH_UNITS:
+                continue  # a length the user gave in another unit: never mix in the default's unit
             _merge_defaults(cfg[k], dv)
     return cfg
 

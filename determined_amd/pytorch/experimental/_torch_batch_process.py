@@ -138,13 +138,14 @@ def _checkpoint_progress(core_context: Any, steps_completed: int, output_uuid: s
                 json.dump({"batch_completed": done}, f)
 
 
-def _reduce_metrics(ctx: TorchBatchProcessorContext, core_context: Any, steps_completed: int) -> None:
+def _reduce_metrics(ctx: TorchBatchProcessorContext, core_context: Any, steps_completed: int) -> Dict[str, Any]:
     wrapped = list(ctx._wrapped_reducers) if hasattr(ctx, "_wrapped_reducers") else []
     if not wrapped:
-        return
+        return {}
     metrics = ctx.reduce_metrics(for_training=False)
     if core_context.distributed.get_rank() == 0 and metrics:
         core_context.train.report_validation_metrics(steps_completed=steps_completed, metrics=metrics)
+    return metrics or {}
 
 
 def _validate_dataloader_kwargs(kw: Dict[str, Any], batch_size: Optional[int]) -> None:
@@ -215,4 +216,11 @@ def torch_batch_process(batch_processor_cls: Type[TorchBatchProcessor], dataset:
             processor.on_checkpoint_start()
             _checkpoint_progress(core_context, total, output_uuid)
         processor.on_finish()
-        _reduce_metrics(ctx, core_context, steps)
+        metrics = _reduce_metrics(ctx, core_context, steps)
+        if info is not None and info.task_type == "TRIAL":
+            # close the trial's searcher operation(s) so the master does not reschedule a task
+            # whose work is done (every rank takes part: the ops are a collective)
+            value = next(iter(metrics.values()), 0.0) if metrics else 0.0
+            for op in core_context.searcher.operations():
+                if rank == 0:
+                    op.report_completed(float(value) if isinstance(value, (int, float)) else 0.0)
