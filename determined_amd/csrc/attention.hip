@@ -21,8 +21,13 @@
 //   S = Q.K^T and dP = dO.V^T with the key on the lane (K, V fragments of the wave's keys stay
 //   in registers), P = exp2(S.scale.log2e - LSE.log2e), dS = P.(dP - delta); P / dS feed
 //   dV^T = dO^T.P and dK^T = Q^T.dS directly (dO^T, Q^T by transposed reads of the row-major
-//   tiles); dS crosses LDS once for dQ = dS.K, summed into an fp32 buffer with float atomics
-//   and converted to bf16 by a final pass.
+//   tiles).
+// dQ (separate kernel, query-major like the forward): S^T = K.Q^T and dP^T = V.dO^T, P^T from
+//   the saved LSE, dS^T = P^T.(dP^T - delta), dQ^T += K^T.dS^T, written once as bf16.  Summing
+//   dQ over key blocks with float atomics instead (one 64x64 fp32 tile per key/query block
+//   pair: ~285 MB of atomic adds per GPT-2-medium layer at mb 8) ran at the chip's atomic rate
+//   and made the backward atomic-bound; recomputing S and dP costs two extra MFMA tiles per
+//   block pair and no atomics.
 //
 // Strides are in elements for (batch, head, token); the head dimension must be contiguous.
 
@@ -291,11 +296,9 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
-  constexpr int RP = D + 8, SP = kBlk + 8;
+  constexpr int RP = D + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[kBlk * RP];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[kBlk * RP];
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * RP];  // this workgroup's keys
-  __shared__ __attribute__((aligned(16))) bf16_t dSs[kBlk * SP];  // [q][key]
   __shared__ float lse2[kBlk], dl[kBlk];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
@@ -319,11 +322,6 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
     }
     kf[ds] = x;
     vf[ds] = y;
-  }
-  {
-    Stage<D, kBlk> kst;
-    kst.load(Kp, a.sk.t, k0, T);
-    kst.store(Ks);
   }
   f4 dk[D / 16], dv[D / 16];
 #pragma unroll
@@ -381,35 +379,6 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
         dk[dt] = mfma(tr_pair(Qs, RP, s2 * 32 + 4 * g, s2 * 32 + 16 + 4 * g, dt * 16, c), sb, dk[dt]);
       }
     }
-    // dS -> LDS [q][key] for dQ = dS . K
-#pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dSs[(qt * 16 + 4 * g + r) * SP + w * 16 + c] = static_cast<bf16_t>(bfs(dS[qt][r]));
-    }
-    __syncthreads();
-    f4 dq[D / 16];
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) dq[dt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const s8 sa = *reinterpret_cast<const s8*>(dSs + (w * 16 + c) * SP + ks * 32 + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        // B = K[key = ks*32 + 8g + j][d = dt*16 + c]: natural k order, two transposed reads
-        const s8 kt = tr_pair(Ks, RP, ks * 32 + 8 * g, ks * 32 + 8 * g + 4, dt * 16, c);
-        dq[dt] = mfma(sa, kt, dq[dt]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = q0 + w * 16 + 4 * g + r;
-      if (q < T) {
-        float* dst = a.dq_acc + (bh * T + q) * D + c;
-#pragma unroll
-        for (int dt = 0; dt < D / 16; ++dt) atomicAdd(dst + dt * 16, dq[dt][r] * a.scale);
-      }
-    }
   }
   if (mykey < T) {
     bf16_t* dKp = a.dk + b * a.sdk.b + h * a.sdk.h + static_cast<int64_t>(mykey) * a.sdk.t;
@@ -428,24 +397,133 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
   }
 }
 
-// dq[b,t,h,:] (strided bf16) = dq_acc[b,h,t,:] (fp32, contiguous)
-template <int D>
-__global__ void __launch_bounds__(256) attn_dq_convert_kernel(const float* __restrict__ acc, bf16_t* __restrict__ dq,
-                                                              Strides s, int H, int T, int64_t n8) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= n8) return;
-  const int64_t e = i * 8;
-  const int d = static_cast<int>(e % D);
-  const int64_t row = e / D;
-  const int t = static_cast<int>(row % T);
-  const int64_t bh = row / T;
-  const int h = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
-  const float4 x0 = *reinterpret_cast<const float4*>(acc + e);
-  const float4 x1 = *reinterpret_cast<const float4*>(acc + e + 4);
-  s8 o;
-  o[0] = bfs(x0.x); o[1] = bfs(x0.y); o[2] = bfs(x0.z); o[3] = bfs(x0.w);
-  o[4] = bfs(x1.x); o[5] = bfs(x1.y); o[6] = bfs(x1.z); o[7] = bfs(x1.w);
-  *reinterpret_cast<s8*>(dq + b * s.b + h * s.h + t * s.t + d) = o;
+struct DqArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dout;
+  const float* lse; const float* delta; bf16_t* dq;
+  Strides sq, sk, sv, sdo, sdq;
+  int H, T;
+  float scale, scale_log2;
+};
+
+// dQ for a block of kFwdRows query rows (same wave / lane layout as the forward).
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
+  constexpr int KP = D + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[kBlk * KP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int T = a.T, nkb = (T + kBlk - 1) / kBlk, nqb = (T + kFwdRows - 1) / kFwdRows;
+  const int qb = CAUSAL ? (nqb - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = qb * kFwdRows, qw = q0 + w * 16 * kQT;
+  const int64_t bh = static_cast<int64_t>(b) * a.H + h;
+  const bf16_t* Qp = a.q + b * a.sq.b + h * a.sq.h;
+  const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
+  const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
+  const bf16_t* dOp = a.dout + b * a.sdo.b + h * a.sdo.h;
+
+  s8 qf[kQT][D / 32], of[kQT][D / 32];
+  float lse2[kQT], dl[kQT];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int q = qw + qt * 16 + c;
+#pragma unroll
+    for (int ds = 0; ds < D / 32; ++ds) {
+      s8 x = {0, 0, 0, 0, 0, 0, 0, 0}, y = x;
+      if (q < T) {
+        x = *reinterpret_cast<const s8*>(Qp + static_cast<int64_t>(q) * a.sq.t + ds * 32 + 8 * g);
+        y = *reinterpret_cast<const s8*>(dOp + static_cast<int64_t>(q) * a.sdo.t + ds * 32 + 8 * g);
+      }
+      qf[qt][ds] = x;
+      of[qt][ds] = y;
+    }
+    lse2[qt] = q < T ? a.lse[bh * T + q] * kLog2e : INFINITY;
+    dl[qt] = q < T ? a.delta[bh * T + q] : 0.f;
+  }
+  f4 dq[kQT][D / 16];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) dq[qt][dt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int kb_end = CAUSAL ? min(nkb, (q0 + kFwdRows - 1) / kBlk + 1) : nkb;
+  Stage<D, kBlk> ks, vs;
+  ks.load(Kp, a.sk.t, 0, T);
+  vs.load(Vp, a.sv.t, 0, T);
+  for (int kb = 0; kb < kb_end; ++kb) {
+    const int k0 = kb * kBlk;
+    __syncthreads();
+    ks.store(Ks);
+    vs.store(Vs);
+    __syncthreads();
+    if (kb + 1 < kb_end) {
+      ks.load(Kp, a.sk.t, k0 + kBlk, T);
+      vs.load(Vp, a.sv.t, k0 + kBlk, T);
+    }
+    // S^T = K.Q^T and dP^T = V.dO^T (key on the accumulator rows, query on the lane)
+    f4 s[kQT][4], dp[kQT][4];
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) s[qt][nt] = dp[qt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int ds = 0; ds < D / 32; ++ds) {
+        const s8 kf = *reinterpret_cast<const s8*>(Ks + (nt * 16 + c) * KP + ds * 32 + 8 * g);
+        const s8 vf = *reinterpret_cast<const s8*>(Vs + (nt * 16 + c) * KP + ds * 32 + 8 * g);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt) {
+          s[qt][nt] = mfma(kf, qf[qt][ds], s[qt][nt]);
+          dp[qt][nt] = mfma(vf, of[qt][ds], dp[qt][nt]);
+        }
+      }
+    }
+    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && k0 + kBlk - 1 > qw);
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt) {
+      const int myq = qw + qt * 16 + c;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = exp2f(s[qt][nt][r] * a.scale_log2 - lse2[qt]);
+          if (need_mask) {
+            const int key = k0 + nt * 16 + 4 * g + r;
+            if (key >= T || (CAUSAL && key > myq)) p = 0.f;
+          }
+          s[qt][nt][r] = p * (dp[qt][nt][r] - dl[qt]);  // dS^T
+        }
+      }
+    }
+    // dQ^T += K^T . dS^T (32 keys per step in the permuted order of the forward's V^T.P^T)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s8 sb[kQT];
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) sb[qt] = pack_pair(s[qt][2 * s2], s[qt][2 * s2 + 1]);
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const s8 kt = tr_pair(Ks, KP, s2 * 32 + 4 * g, s2 * 32 + 16 + 4 * g, dt * 16, c);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt) dq[qt][dt] = mfma(kt, sb[qt], dq[qt][dt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int myq = qw + qt * 16 + c;
+    if (myq < T) {
+      bf16_t* Dp = a.dq + b * a.sdq.b + h * a.sdq.h + static_cast<int64_t>(myq) * a.sdq.t;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        s4 ov;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = bfs(dq[qt][dt][r] * a.scale);
+        *reinterpret_cast<s4*>(Dp + dt * 16 + 4 * g) = ov;
+      }
+    }
+  }
 }
 
 }  // namespace attn
@@ -483,7 +561,7 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   const Strides sq{s[0], s[1], s[2]}, sk{s[3], s[4], s[5]}, sv{s[6], s[7], s[8]}, so{s[9], s[10], s[11]},
       sdo{s[12], s[13], s[14]}, sdk{s[15], s[16], s[17]}, sdv{s[18], s[19], s[20]}, sdq{s[21], s[22], s[23]};
   const int64_t rows = static_cast<int64_t>(B) * H * T;
-  (void)hipMemsetAsync(dq_acc, 0, sizeof(float) * rows * D, st);
+  (void)dq_acc;  // unused: dQ is produced by attn_dq_kernel without an fp32 accumulator
   {
     const int64_t threads = rows * (D / 8);
     const int blocks = static_cast<int>((threads + 255) / 256);
@@ -510,14 +588,19 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
     else hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
   }
   DAMD_CHECK_LAUNCH();
-  const int64_t n8 = rows * D / 8;
-  const int blocks = static_cast<int>((n8 + 255) / 256);
-  if (D == 64)
-    hipLaunchKernelGGL((attn_dq_convert_kernel<64>), dim3(blocks), dim3(256), 0, st, dq_acc,
-                       static_cast<bf16_t*>(dq), sdq, H, T, n8);
-  else
-    hipLaunchKernelGGL((attn_dq_convert_kernel<128>), dim3(blocks), dim3(256), 0, st, dq_acc,
-                       static_cast<bf16_t*>(dq), sdq, H, T, n8);
+  DqArgs d;
+  d.q = a.q; d.k = a.k; d.v = a.v; d.dout = a.dout; d.lse = lse; d.delta = delta;
+  d.dq = static_cast<bf16_t*>(dq);
+  d.sq = sq; d.sk = sk; d.sv = sv; d.sdo = sdo; d.sdq = sdq;
+  d.H = H; d.T = T; d.scale = scale; d.scale_log2 = scale * kLog2e;
+  dim3 qgrid((T + kFwdRows - 1) / kFwdRows, H, B);
+  if (D == 64) {
+    if (causal) hipLaunchKernelGGL((attn_dq_kernel<64, true>), qgrid, dim3(kThreads), 0, st, d);
+    else hipLaunchKernelGGL((attn_dq_kernel<64, false>), qgrid, dim3(kThreads), 0, st, d);
+  } else {
+    if (causal) hipLaunchKernelGGL((attn_dq_kernel<128, true>), qgrid, dim3(kThreads), 0, st, d);
+    else hipLaunchKernelGGL((attn_dq_kernel<128, false>), qgrid, dim3(kThreads), 0, st, d);
+  }
   DAMD_CHECK_LAUNCH();
 }
 

@@ -577,13 +577,13 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   const int64_t B = q.size(0), H = q.size(1), T = q.size(2), D = q.size(3);
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse [B,H,T] f32");
   auto delta = at::empty({B, H, T}, lse.options());
-  auto dq_acc = at::empty({B, H, T, D}, lse.options());
+
   std::vector<int64_t> s;
   const at::Tensor* order[] = {&q, &k, &v, &o, &dout, &dk, &dv, &dq};
   for (const at::Tensor* t : order) push_strides(s, *t);
   if (B * H * T > 0)
     damd_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
-                         lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(), dq.data_ptr(),
+                         lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr, dq.data_ptr(),
                          dk.data_ptr(), dv.data_ptr(), s.data(), static_cast<int>(B), static_cast<int>(H),
                          static_cast<int>(T), static_cast<int>(D), static_cast<float>(scale), causal ? 1 : 0,
                          cur_stream());

@@ -457,43 +457,63 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
   }
 }
 
-// d(relu output) at input (n, h, w), channels cg*8..+8, gathered from the pooled gradient
+// Pooled gradient routed back to the 2x2 input quad (2oh..2oh+1, 2ow..2ow+1) of output
+// position (oh, ow): the quad's pixels lie in windows (oh..oh+1, ow..ow+1) only (stride 2), so
+// the four (dp, argmax) vectors are loaded once per quad instead of once per input pixel.
+// dr[2*i + j] is the gradient of input (2oh + i, 2ow + j).
 template <typename T>
-__device__ __forceinline__ void pool_grad_gather(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int64_t n,
-                                                 int h, int w, int cg, int C, const PoolGeo& g, float* dr) {
+__device__ __forceinline__ void quad_pool_grad(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int64_t n,
+                                               int oh, int ow, int cg, int C, const PoolGeo& g, float (*dr)[8]) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) dr[k] = 0.f;
-  const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, g.OH - 1);
-  const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, g.OW - 1);
-  for (int oh = oh0; oh <= oh1; ++oh) {
-    for (int ow = ow0; ow <= ow1; ++ow) {
-      const int64_t o = ((n * g.OH + oh) * g.OW + ow) * C + cg * 8;
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dr[p][k] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int wh = oh + a;
+    if (wh >= g.OH) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ww = ow + b;
+      if (ww >= g.OW) continue;
+      const int64_t o = ((n * g.OH + wh) * g.OW + ww) * C + cg * 8;
       const uint2 ii = *reinterpret_cast<const uint2*>(idx + o);
-      const int pos = win_pos(h, w, oh, ow);
       float d[8];
       V8<T>::ld(dp + o, d);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (static_cast<int>((ii.x >> (8 * k)) & 0xFFu) == pos) dr[k] += d[k];
-        if (static_cast<int>((ii.y >> (8 * k)) & 0xFFu) == pos) dr[k + 4] += d[k + 4];
+      for (int i = 0; i < 2; ++i) {
+        const int kh = 2 * oh + i - 2 * wh + 1;  // row of input 2oh+i inside window wh
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int kw = 2 * ow + j - 2 * ww + 1;
+          if (kw < 0 || kw > 2) continue;
+          const uint32_t pos = static_cast<uint32_t>(kh * 3 + kw);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (((ii.x >> (8 * k)) & 0xFFu) == pos) dr[2 * i + j][k] += d[k];
+            if (((ii.y >> (8 * k)) & 0xFFu) == pos) dr[2 * i + j][k + 4] += d[k + 4];
+          }
+        }
       }
     }
   }
 }
 
-// BN-backward reduce over dz = maxpool_bwd(dp) * [bn(x) > 0]: part[nb][2][C] = (sum dz, sum dz*(x-mean))
+// BN-backward reduce over dz = maxpool_bwd(dp) * [bn(x) > 0]: part[nb][2][C] = (sum dz, sum dz*(x-mean)).
+// Rows of this kernel are output positions (quads of 4 input pixels).
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
 maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
                              const float* __restrict__ mean, const float* __restrict__ scale,
-                             const float* __restrict__ shift, int64_t M, int C, int64_t rows_per_block,
+                             const float* __restrict__ shift, int64_t Q, int C, int64_t rows_per_block,
                              float* __restrict__ part, PoolGeo g) {
   const Geo geo_ = geo(C);
   const int tid = threadIdx.x;
   const int cg0 = geo_.TPR <= kBNThreads ? tid % geo_.TPR : tid;
   const int rsub = geo_.TPR <= kBNThreads ? tid / geo_.TPR : 0;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int64_t r1 = min(Q, r0 + rows_per_block);
   __shared__ float red[kBNThreads * 8];
   for (int gi = 0; gi < geo_.G; ++gi) {
     const int cg = cg0 + gi * kBNThreads;
@@ -503,18 +523,29 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict
     V8<float>::ld(shift + cg * 8, sh);
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s[k] = 0.f; sx[k] = 0.f; }
-    for (int64_t r = r0 + rsub; r < r1; r += geo_.RS) {
-      const int w = static_cast<int>(r % g.W);
-      const int h = static_cast<int>((r / g.W) % g.H);
-      const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
-      float a[8], dr[8];
-      V8<T>::ld(x + r * C + cg * 8, a);
-      pool_grad_gather(dp, idx, n, h, w, cg, C, g, dr);
+    for (int64_t q = r0 + rsub; q < r1; q += geo_.RS) {
+      const int ow = static_cast<int>(q % g.OW);
+      const int oh = static_cast<int>((q / g.OW) % g.OH);
+      const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
+      float dr[4][8];
+      quad_pool_grad(dp, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[k] : 0.f;
-        s[k] += dz;
-        sx[k] += dz * (a[k] - mu[k]);
+      for (int i = 0; i < 2; ++i) {
+        const int h = 2 * oh + i;
+        if (h >= g.H) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int w = 2 * ow + j;
+          if (w >= g.W) continue;
+          float a[8];
+          V8<T>::ld(x + ((n * g.H + h) * g.W + w) * C + cg * 8, a);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[2 * i + j][k] : 0.f;
+            s[k] += dz;
+            sx[k] += dz * (a[k] - mu[k]);
+          }
+        }
       }
     }
     for (int which = 0; which < 2; ++which) {
@@ -525,9 +556,9 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict
         for (int k = 0; k < 8; ++k) red[tid * 8 + k] = v[k];
         __syncthreads();
         if (rsub == 0) {
-          for (int q = 1; q < geo_.RS; ++q)
+          for (int qq = 1; qq < geo_.RS; ++qq)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += red[(q * geo_.TPR + cg0) * 8 + k];
+            for (int k = 0; k < 8; ++k) v[k] += red[(qq * geo_.TPR + cg0) * 8 + k];
         }
       }
       if (rsub == 0) V8<float>::st(part + (static_cast<int64_t>(blockIdx.x) * 2 + which) * C + cg * 8, v);
@@ -535,11 +566,12 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict
   }
 }
 
+// dx = A*dz + B*x + Cc over one quad of input pixels per (output position, channel group)
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
 maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
                             const float* __restrict__ scale, const float* __restrict__ shift,
-                            const float* __restrict__ coef, int C, T* __restrict__ dx, int64_t V, int TPR, PoolGeo g) {
+                            const float* __restrict__ coef, int C, T* __restrict__ dx, int64_t VQ, int TPR, PoolGeo g) {
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
   const int cg = static_cast<int>(T0 % TPR);
@@ -549,20 +581,32 @@ maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const uint8_t* __restrict_
   V8<float>::ld(coef + 2 * C + cg * 8, Cc);
   V8<float>::ld(scale + cg * 8, sc);
   V8<float>::ld(shift + cg * 8, sh);
-  for (int64_t v = T0; v < V; v += stride) {
-    const int64_t r = v / TPR;
-    const int w = static_cast<int>(r % g.W);
-    const int h = static_cast<int>((r / g.W) % g.H);
-    const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
-    float a[8], dr[8], o[8];
-    V8<T>::ld(x + v * 8, a);
-    pool_grad_gather(dp, idx, n, h, w, cg, C, g, dr);
+  for (int64_t v = T0; v < VQ; v += stride) {
+    const int64_t q = v / TPR;
+    const int ow = static_cast<int>(q % g.OW);
+    const int oh = static_cast<int>((q / g.OW) % g.OH);
+    const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
+    float dr[4][8];
+    quad_pool_grad(dp, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[k] : 0.f;
-      o[k] = A[k] * dz + B[k] * a[k] + Cc[k];
+    for (int i = 0; i < 2; ++i) {
+      const int h = 2 * oh + i;
+      if (h >= g.H) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int w = 2 * ow + j;
+        if (w >= g.W) continue;
+        const int64_t off = ((n * g.H + h) * g.W + w) * C + cg * 8;
+        float a[8], o[8];
+        V8<T>::ld(x + off, a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? dr[2 * i + j][k] : 0.f;
+          o[k] = A[k] * dz + B[k] * a[k] + Cc[k];
+        }
+        V8<T>::st(dx + off, o);
+      }
     }
-    V8<T>::st(dx + v * 8, o);
   }
 }
 
@@ -744,16 +788,17 @@ void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, 
                              int OW, const float* mean, const float* invstd, const float* scale, const float* shift,
                              float* part, float* coef, void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype,
                              hipStream_t st) {
-  const int64_t M = N * H * W;
+  const int64_t M = N * H * W;      // BN statistics count
+  const int64_t Q = N * OH * OW;    // quads (rows of the fused backward kernels)
   int nb;
-  const int64_t rpb = rows_per_block_for(M, C, &nb);
+  const int64_t rpb = rows_per_block_for(Q, C, &nb);
   const PoolGeo g{H, W, OH, OW};
   if (x_dtype == 1)
     hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
-                       static_cast<const bf16_t*>(x), mean, scale, shift, M, C, rpb, part, g);
+                       static_cast<const bf16_t*>(x), mean, scale, shift, Q, C, rpb, part, g);
   else
     hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
-                       static_cast<const float*>(x), mean, scale, shift, M, C, rpb, part, g);
+                       static_cast<const float*>(x), mean, scale, shift, Q, C, rpb, part, g);
   if (w_dtype == 1)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
@@ -761,13 +806,13 @@ void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, 
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   const int TPR = C / 8;
-  const int64_t V = M * TPR;
-  const dim3 ag(apply_grid(V, TPR));
+  const int64_t VQ = Q * TPR;
+  const dim3 ag(apply_grid(VQ, TPR));
   if (x_dtype == 1)
     hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
-                       static_cast<const bf16_t*>(x), scale, shift, coef, C, static_cast<bf16_t*>(dx), V, TPR, g);
+                       static_cast<const bf16_t*>(x), scale, shift, coef, C, static_cast<bf16_t*>(dx), VQ, TPR, g);
   else
     hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
-                       static_cast<const float*>(x), scale, shift, coef, C, static_cast<float*>(dx), V, TPR, g);
+                       static_cast<const float*>(x), scale, shift, coef, C, static_cast<float*>(dx), VQ, TPR, g);
   DAMD_CHECK_LAUNCH();
 }
