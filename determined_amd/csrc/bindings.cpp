@@ -64,12 +64,12 @@ void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, co
                                hipStream_t);
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
                         const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
-                        hipStream_t, const uint8_t*);
+                        hipStream_t, const uint8_t*, const void*);
 void damd_bn_pool_fwd_launch(const void*, void*, uint8_t*, int64_t, int, int, int, int, int, const void*, const void*,
                              float*, float*, float, float, float*, float*, float*, float*, float*, int, int, hipStream_t);
 void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, int, int, int, int, int, const float*,
                              const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
-                             hipStream_t);
+                             hipStream_t, const void*);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
                                      int, int, float, int, hipStream_t);
@@ -368,7 +368,7 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
 std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
                                    const c10::optional<at::Tensor>& residual, const at::Tensor& stats,
                                    const at::Tensor& weight, bool relu, bool need_dres,
-                                   const c10::optional<at::Tensor>& mask) {
+                                   const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& dy2) {
   check_bn_tensor(dy, x, "dy");
   const int64_t C = bn_channels(x);
   const int64_t M = x.numel() / C;
@@ -382,6 +382,13 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
     TORCH_CHECK(relu && mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() == M * C / 8 &&
                 mask->device() == x.device(), "bn_act_bwd: mask must be a uint8 [M*C/8] tensor (ReLU path)");
     mp = mask->data_ptr<uint8_t>();
+  }
+  // dy2: gradient of the output's second consumer (ops/bn.py split_grad), summed in-kernel
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    TORCH_CHECK(mp != nullptr, "bn_act_bwd: a second gradient needs the masked ReLU path");
+    check_bn_tensor(*dy2, x, "dy2");
+    d2 = dy2->data_ptr();
   }
   auto fopts = x.options().dtype(at::kFloat);
   const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
@@ -397,7 +404,7 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
                      stats[1].data_ptr<float>(), stats[2].data_ptr<float>(), stats[3].data_ptr<float>(),
                      part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(),
                      dx.data_ptr(), write_dres ? dres.data_ptr() : nullptr, relu, dtype_code(x), dtype_code(weight),
-                     cur_stream(), mp);
+                     cur_stream(), mp, d2);
   return {dx, dgamma, dbeta, dres};
 }
 
@@ -494,7 +501,8 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
 }
 
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& x,
-                                    const at::Tensor& stats, const at::Tensor& weight) {
+                                    const at::Tensor& stats, const at::Tensor& weight,
+                                    const c10::optional<at::Tensor>& dp2) {
   TORCH_CHECK(x.dim() == 4 && bn_supported(x), "bn_pool_bwd: bad x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
@@ -509,11 +517,18 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx,
   auto dgamma = at::empty({C}, weight.options());
   auto dbeta = at::empty({C}, weight.options());
   auto dx = at::empty_like(x);
+  const void* d2 = nullptr;
+  if (dp2.has_value() && dp2->defined()) {
+    TORCH_CHECK(dp2->sizes() == dp.sizes() && dp2->strides() == dp.strides() &&
+                dp2->scalar_type() == dp.scalar_type() && dp2->device() == dp.device(),
+                "bn_pool_bwd: dp2 must match dp");
+    d2 = dp2->data_ptr();
+  }
   damd_bn_pool_bwd_launch(dp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), N, static_cast<int>(H),
                           static_cast<int>(W), static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW),
                           stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
                           stats[3].data_ptr<float>(), part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(),
-                          dbeta.data_ptr(), dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream());
+                          dbeta.data_ptr(), dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream(), d2);
   return {dx, dgamma, dbeta};
 }
 

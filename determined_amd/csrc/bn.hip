@@ -237,15 +237,26 @@ bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ scale, const 
 }
 
 // ----------------------------------------------------------------------------- bwd reduce
+template <typename T>
+__device__ __forceinline__ void add_v8(const T* __restrict__ p, float* d) {
+  float e[8];
+  V8<T>::ld(p, e);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] += e[k];
+}
+
 // part: [nb][2][C] = (sum dy', sum dy' * (x - mean))
 // MASKED: the ReLU mask comes from the forward's bit mask instead of recomputing it from
 // x (and the residual), see bn_apply_kernel<..., WMASK>.
-template <typename T, bool RES, bool RELU, bool MASKED = false>
+// DY2: the output fed two consumers and dy2 holds the second one's gradient; the two are
+// summed on the fly instead of in a separate elementwise add (see ops/bn.py split_grad).
+template <typename T, bool RES, bool RELU, bool MASKED = false, bool DY2 = false>
 __global__ void __launch_bounds__(kBNThreads)
 bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
                      const float* __restrict__ mean, const float* __restrict__ scale,
                      const float* __restrict__ shift, int64_t M, int C, int64_t rows_per_block,
-                     float* __restrict__ part, const uint8_t* __restrict__ mask = nullptr) {
+                     float* __restrict__ part, const uint8_t* __restrict__ mask = nullptr,
+                     const T* __restrict__ dy2 = nullptr) {
   const Geo g = geo(C);
   const int tid = threadIdx.x;
   const int cg0 = g.TPR <= kBNThreads ? tid % g.TPR : tid;
@@ -268,6 +279,7 @@ bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T*
       for (int u = 0; u < 2; ++u) {
         const int64_t off = (r + u * g.RS) * C + cg * 8;
         V8<T>::ld(dy + off, d[u]);
+        if (DY2) add_v8(dy2 + off, d[u]);
         V8<T>::ld(x + off, a[u]);
         if (MASKED) mb[u] = mask[off >> 3];
         else if (RES && RELU) V8<T>::ld(res + off, rr[u]);
@@ -293,6 +305,7 @@ bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T*
       uint32_t mb = 0u;
       const int64_t off = r * C + cg * 8;
       V8<T>::ld(dy + off, d);
+      if (DY2) add_v8(dy2 + off, d);
       V8<T>::ld(x + off, a);
       if (MASKED) mb = mask[off >> 3];
       else if (RES && RELU) V8<T>::ld(res + off, rr);
@@ -357,12 +370,12 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
   }
 }
 
-template <typename T, bool RES, bool RELU, bool WRITE_DRES, bool MASKED = false>
+template <typename T, bool RES, bool RELU, bool WRITE_DRES, bool MASKED = false, bool DY2 = false>
 __global__ void __launch_bounds__(kBNThreads)
 bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ res,
                     const float* __restrict__ scale, const float* __restrict__ shift,
                     const float* __restrict__ coef, int C, T* __restrict__ dx, T* __restrict__ dres, int64_t V,
-                    int TPR, const uint8_t* __restrict__ mask = nullptr) {
+                    int TPR, const uint8_t* __restrict__ mask = nullptr, const T* __restrict__ dy2 = nullptr) {
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
   const int cg = static_cast<int>(T0 % TPR);
@@ -375,6 +388,7 @@ bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x, const T* 
     float d[8], a[8], rr[8], o[8];
     uint32_t mb = 0u;
     V8<T>::ld(dy + v * 8, d);
+    if (DY2) add_v8(dy2 + v * 8, d);
     V8<T>::ld(x + v * 8, a);
     if (MASKED) mb = mask[v];
     else if (RES && RELU) V8<T>::ld(res + v * 8, rr);
@@ -462,8 +476,9 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
 // the four (dp, argmax) vectors are loaded once per quad instead of once per input pixel.
 // dr[2*i + j] is the gradient of input (2oh + i, 2ow + j).
 template <typename T>
-__device__ __forceinline__ void quad_pool_grad(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int64_t n,
-                                               int oh, int ow, int cg, int C, const PoolGeo& g, float (*dr)[8]) {
+__device__ __forceinline__ void quad_pool_grad(const T* __restrict__ dp, const T* __restrict__ dp2,
+                                               const uint8_t* __restrict__ idx, int64_t n, int oh, int ow, int cg,
+                                               int C, const PoolGeo& g, float (*dr)[8]) {
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -480,6 +495,7 @@ __device__ __forceinline__ void quad_pool_grad(const T* __restrict__ dp, const u
       const uint2 ii = *reinterpret_cast<const uint2*>(idx + o);
       float d[8];
       V8<T>::ld(dp + o, d);
+      if (dp2 != nullptr) add_v8(dp2 + o, d);  // pooled output fed two consumers
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int kh = 2 * oh + i - 2 * wh + 1;  // row of input 2oh+i inside window wh
@@ -504,7 +520,7 @@ __device__ __forceinline__ void quad_pool_grad(const T* __restrict__ dp, const u
 // Rows of this kernel are output positions (quads of 4 input pixels).
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
-maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
+maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ dp2, const uint8_t* __restrict__ idx, const T* __restrict__ x,
                              const float* __restrict__ mean, const float* __restrict__ scale,
                              const float* __restrict__ shift, int64_t Q, int C, int64_t rows_per_block,
                              float* __restrict__ part, PoolGeo g) {
@@ -528,7 +544,7 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict
       const int oh = static_cast<int>((q / g.OW) % g.OH);
       const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
       float dr[4][8];
-      quad_pool_grad(dp, idx, n, oh, ow, cg, C, g, dr);
+      quad_pool_grad(dp, dp2, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int h = 2 * oh + i;
@@ -569,7 +585,7 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const uint8_t* __restrict
 // dx = A*dz + B*x + Cc over one quad of input pixels per (output position, channel group)
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
-maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ x,
+maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const T* __restrict__ dp2, const uint8_t* __restrict__ idx, const T* __restrict__ x,
                             const float* __restrict__ scale, const float* __restrict__ shift,
                             const float* __restrict__ coef, int C, T* __restrict__ dx, int64_t VQ, int TPR, PoolGeo g) {
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
@@ -587,7 +603,7 @@ maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const uint8_t* __restrict_
     const int oh = static_cast<int>((q / g.OW) % g.OH);
     const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
     float dr[4][8];
-    quad_pool_grad(dp, idx, n, oh, ow, cg, C, g, dr);
+    quad_pool_grad(dp, dp2, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int h = 2 * oh + i;
@@ -700,17 +716,17 @@ void damd_bn_apply_only_launch(const void* x, const void* res, void* y, int64_t 
 void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t M, int C, const float* mean,
                         const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                         void* dgamma, void* dbeta, void* dx, void* dres, int relu, int x_dtype, int w_dtype,
-                        hipStream_t st, const uint8_t* mask) {
+                        hipStream_t st, const uint8_t* mask, const void* dy2) {
   int nb;
   const int64_t rpb = rows_per_block_for(M, C, &nb);
   const bool has_res = res != nullptr || mask != nullptr;
   const bool masked = mask != nullptr && relu;
 #define RED(T, R, A) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part, nullptr)
+  // a second gradient (dy2) is only taken on the masked residual path (ResNet block outputs)
+#define REDM(T, D2) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true, true, D2>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask, static_cast<const T*>(dy2))
   if (masked) {
-    if (x_dtype == 1)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, true, true, true>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, true, true, true>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dy), static_cast<const float*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask);
+    if (x_dtype == 1) { if (dy2) REDM(bf16_t, true); else REDM(bf16_t, false); }
+    else { if (dy2) REDM(float, true); else REDM(float, false); }
   } else if (x_dtype == 1) {
     if (has_res) { if (relu) RED(bf16_t, true, true); else RED(bf16_t, true, false); }
     else { if (relu) RED(bf16_t, false, true); else RED(bf16_t, false, false); }
@@ -719,6 +735,7 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
     else { if (relu) RED(float, false, true); else RED(float, false, false); }
   }
 #undef RED
+#undef REDM
   if (w_dtype == 1)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
@@ -730,10 +747,15 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   const dim3 ag(apply_grid(V, TPR));
   const bool wd = dres != nullptr;
 #define BAP(T, R, A, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, nullptr)
-#define BAPM(T, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true, W, true>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, mask)
+#define BAPM(T, W, D2) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true, W, true, D2>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, mask, static_cast<const T*>(dy2))
   if (masked) {
-    if (x_dtype == 1) { if (wd) BAPM(bf16_t, true); else BAPM(bf16_t, false); }
-    else { if (wd) BAPM(float, true); else BAPM(float, false); }
+    if (x_dtype == 1) {
+      if (dy2) { if (wd) BAPM(bf16_t, true, true); else BAPM(bf16_t, false, true); }
+      else { if (wd) BAPM(bf16_t, true, false); else BAPM(bf16_t, false, false); }
+    } else {
+      if (dy2) { if (wd) BAPM(float, true, true); else BAPM(float, false, true); }
+      else { if (wd) BAPM(float, true, false); else BAPM(float, false, false); }
+    }
   } else if (x_dtype == 1) {
     if (has_res) { if (relu) { if (wd) BAP(bf16_t, true, true, true); else BAP(bf16_t, true, true, false); }
                    else { if (wd) BAP(bf16_t, true, false, true); else BAP(bf16_t, true, false, false); } }
@@ -787,17 +809,17 @@ void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, in
 void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, int64_t N, int H, int W, int C, int OH,
                              int OW, const float* mean, const float* invstd, const float* scale, const float* shift,
                              float* part, float* coef, void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype,
-                             hipStream_t st) {
+                             hipStream_t st, const void* dp2) {
   const int64_t M = N * H * W;      // BN statistics count
   const int64_t Q = N * OH * OW;    // quads (rows of the fused backward kernels)
   int nb;
   const int64_t rpb = rows_per_block_for(Q, C, &nb);
   const PoolGeo g{H, W, OH, OW};
   if (x_dtype == 1)
-    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
                        static_cast<const bf16_t*>(x), mean, scale, shift, Q, C, rpb, part, g);
   else
-    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
                        static_cast<const float*>(x), mean, scale, shift, Q, C, rpb, part, g);
   if (w_dtype == 1)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
@@ -809,10 +831,10 @@ void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, 
   const int64_t VQ = Q * TPR;
   const dim3 ag(apply_grid(VQ, TPR));
   if (x_dtype == 1)
-    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), idx,
+    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
                        static_cast<const bf16_t*>(x), scale, shift, coef, C, static_cast<bf16_t*>(dx), VQ, TPR, g);
   else
-    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), idx,
+    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
                        static_cast<const float*>(x), scale, shift, coef, C, static_cast<float*>(dx), VQ, TPR, g);
   DAMD_CHECK_LAUNCH();
 }

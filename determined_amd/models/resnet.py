@@ -37,11 +37,14 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNormAct2d(cout)  # fused: relu(bn3(conv3) + identity)
         self.downsample = downsample
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+    def forward(self, x, split_grad: bool = False):
+        """``x`` is a tensor or the ``(main, shortcut)`` pair of a split-gradient producer;
+        ``split_grad`` makes this block's output such a pair (ops/bn.py)."""
+        xm, xs = x if isinstance(x, tuple) else (x, x)
+        identity = xs if self.downsample is None else self.downsample(xs)
+        out = self.bn1(self.conv1(xm))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity)
+        return self.bn3(self.conv3(out), identity, split_grad=split_grad)
 
 
 class BasicBlock(nn.Module):
@@ -55,10 +58,11 @@ class BasicBlock(nn.Module):
         self.bn2 = BatchNormAct2d(width)
         self.downsample = downsample
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), identity)
+    def forward(self, x, split_grad: bool = False):
+        xm, xs = x if isinstance(x, tuple) else (x, x)
+        identity = xs if self.downsample is None else self.downsample(xs)
+        out = self.bn1(self.conv1(xm))
+        return self.bn2(self.conv2(out), identity, split_grad=split_grad)
 
 
 class ResNet(nn.Module):
@@ -102,8 +106,13 @@ class ResNet(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # stem BN + ReLU + max-pool in one fused kernel pair (ops/bn.py: forward_maxpool)
-        x = self.bn1.forward_maxpool(self.conv1(x), self.maxpool)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        # Every activation between blocks feeds two consumers (next conv1 + shortcut): producers
+        # hand out split-gradient pairs so the backward sums the two gradients inside the BN
+        # kernels instead of in separate elementwise adds (ops/bn.py).
+        x = self.bn1.forward_maxpool(self.conv1(x), self.maxpool, split_grad=True)
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        for i, blk in enumerate(blocks):
+            x = blk(x, split_grad=i + 1 < len(blocks))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

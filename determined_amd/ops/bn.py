@@ -6,6 +6,11 @@ state-dict keys) whose forward takes an optional residual and applies ReLU in th
 (stats, apply) and 2 backward (reduce, apply) instead of stock PyTorch's 7 HBM passes; with a
 residual the forward also writes a ReLU bit mask so the backward never re-reads the residual.
 CPU tensors / unsupported shapes use the exact PyTorch composition.
+
+``split_grad=True`` returns the output twice, ``(y, y_alias)``, for an output with two consumers
+(a ResNet block output feeds the next block's conv1 and its shortcut).  Both handles share
+storage, but autograd delivers their gradients separately and the backward kernels sum them
+while reading (one HBM pass fewer than autograd's elementwise gradient accumulation).
 """
 
 from typing import Optional
@@ -15,9 +20,19 @@ import torch.nn.functional as F
 from torch import nn
 
 
+def _sum_grads(a, b, mf):
+    """(first, second) gradient for a split-output backward; either may be None."""
+    if a is None:
+        a, b = b, None
+    if a is None:
+        return None, None
+    a = a.contiguous(memory_format=mf)
+    return a, (None if b is None else b.contiguous(memory_format=mf))
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, split=False):
         from determined_amd import ops
 
         # residual + ReLU: the forward also emits a 1-bit-per-element ReLU mask, so the backward
@@ -28,19 +43,25 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, None if masked else residual, stats, weight, mask if masked else None)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        if split:
+            return y, y.detach()
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         from determined_amd import ops
 
         x, residual, stats, weight, mask = ctx.saved_tensors
         mf = torch.channels_last if x.dim() == 4 else torch.contiguous_format
-        dy = dy.contiguous(memory_format=mf)
+        dy, dy2 = _sum_grads(dy, dy2, mf)
+        if dy is None:
+            return (None,) * 10
+        if dy2 is not None and mask is None:  # unmasked path: plain sum
+            dy, dy2 = dy + dy2, None
         dx, dg, db, dres = ops.ext().bn_act_bwd(dy, x, residual, stats, weight, bool(ctx.relu), bool(ctx.has_res),
-                                                mask)
+                                                mask, dy2)
         return (dx, dg, db, None, None,
-                dres if ctx.has_res else None, None, None, None)
+                dres if ctx.has_res else None, None, None, None, None)
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -49,22 +70,26 @@ class _BNReLUPoolFn(torch.autograd.Function):
     two BN-backward passes."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, split=False):
         from determined_amd import ops
 
         y, idx, stats = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum), float(eps))
         ctx.save_for_backward(x, idx, stats, weight)
         ctx.mark_non_differentiable(idx)
+        if split:
+            return y, y.detach()
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         from determined_amd import ops
 
         x, idx, stats, weight = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight)
-        return dx, dg, db, None, None, None, None
+        dy, dy2 = _sum_grads(dy, dy2, torch.channels_last)
+        if dy is None:
+            return (None,) * 8
+        dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight, dy2)
+        return dx, dg, db, None, None, None, None, None
 
 
 def _torch_bn_act(bn: nn.BatchNorm2d, x, residual, relu, momentum):
@@ -109,7 +134,13 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
         self._nbt_host = None
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, split_grad: bool = False):
+        """``relu(bn(x) [+ residual])``; with ``split_grad`` a pair ``(y, y)`` of handles whose
+        gradients are summed inside the fused backward (module docstring)."""
+        y = self._forward(x, residual, split_grad)
+        return y if not split_grad or isinstance(y, tuple) else (y, y)
+
+    def _forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], split: bool):
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
             self._nbt_host = self._nbt() + 1
@@ -125,7 +156,9 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if self.training or not self.track_running_stats:
             rm = self.running_mean if self.track_running_stats else None
             rv = self.running_var if self.track_running_stats else None
-            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act)
+            # the in-kernel gradient sum needs the masked (residual + ReLU) backward
+            split = split and residual is not None and self.act
+            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act, split)
         # eval: fold running statistics; one elementwise pass.
         scale = self.weight.float() * torch.rsqrt(self.running_var + self.eps)
         shift = self.bias.float() - self.running_mean * scale
@@ -136,7 +169,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return F.relu(y) if self.act else y
         return e.bn_apply(x, scale, shift, residual, self.act)
 
-    def forward_maxpool(self, x: torch.Tensor, pool: nn.MaxPool2d) -> torch.Tensor:
+    def forward_maxpool(self, x: torch.Tensor, pool: nn.MaxPool2d, split_grad: bool = False):
         """``pool(self(x))`` with the fused stem kernels when ``pool`` is the ResNet 3x3/s2/p1
         max-pool, training mode and a supported channels-last GPU tensor; exact composition
         otherwise."""
@@ -149,12 +182,14 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
             fusable = ops.ext().bn_supported(x) and x.is_contiguous(memory_format=torch.channels_last)
         if not fusable:
-            return pool(self(x))
+            y = pool(self(x))
+            return (y, y) if split_grad else y
         momentum = 0.0 if self.momentum is None else self.momentum
         self._nbt_host = self._nbt() + 1
         if self.momentum is None:
             momentum = 1.0 / float(self._nbt_host)
-        return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, momentum, self.eps)
+        return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, momentum, self.eps,
+                                   split_grad)
 
     def _apply(self, fn, recurse: bool = True):
         # Running statistics always stay fp32 (a bf16 running_var loses the update signal).

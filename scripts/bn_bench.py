@@ -40,7 +40,7 @@ for H, C, res in SHAPES:
     dy = torch.randn_like(x)
     nbytes = x.numel() * 2
     tf = timeit(lambda: e.bn_act_fwd(x, w, b, rm, rv, 0.1, 1e-5, r, True, True))
-    tb = timeit(lambda: e.bn_act_bwd(dy, x, None if res else None, stats, w, True, res, mask if res else None))
+    tb = timeit(lambda: e.bn_act_bwd(dy, x, None if res else None, stats, w, True, res, mask if res else None, None))
     # compulsory passes: fwd = stats(1R) + apply(1R [+1R res] + 1W); bwd = reduce(2R) + apply(2R + 1W [+1W dres])
     pf = 3 + (1 if res else 0)
     pb = 5 + (1 if res else 0)

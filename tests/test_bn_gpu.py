@@ -130,3 +130,63 @@ def test_bn_relu_maxpool_fused_matches_reference(bnmod, shape, dtype):
     torch.testing.assert_close(m.weight.grad.float(), ref_bn.weight.grad, rtol=2e-2, atol=5e-2)
     torch.testing.assert_close(m.bias.grad.float(), ref_bn.bias.grad, rtol=2e-2, atol=5e-2)
     torch.testing.assert_close(m.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_split_grad_sums_both_consumers(bnmod, dtype):
+    """split_grad: the two handles' gradients are summed inside the BN backward kernels (block
+    output feeding conv + shortcut) -- same result as autograd's accumulation of one output."""
+    torch.manual_seed(0)
+    N, C, H, W = 4, 64, 14, 14
+    m = bnmod.BatchNormAct2d(C).cuda()
+    mk = lambda: torch.randn(N, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    x, res, g1, g2 = mk(), mk(), mk(), mk()
+    xa = x.clone().requires_grad_(True)
+    ra = res.clone().requires_grad_(True)
+    ya, yb = m(xa, ra, split_grad=True)
+    assert ya.data_ptr() == yb.data_ptr()
+    (ya * g1.float()).sum().backward(retain_graph=True)
+    (yb * g2.float()).sum().backward()
+    dga, dba = m.weight.grad.clone(), m.bias.grad.clone()
+    m.zero_grad()
+    xr = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True)
+    y = m(xr, rr)
+    y.backward(g1 + g2 if dtype == torch.float32 else (g1.float() + g2.float()).to(dtype))
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(xa.grad.float(), xr.grad.float(), **tol)
+    torch.testing.assert_close(ra.grad.float(), rr.grad.float(), **tol)
+    # dgamma/dbeta sum ~800 terms (|sum| ~ 40): the unsplit side rounds g1 + g2 to bf16 per
+    # element first, the split side sums in fp32, so bf16 allows that accumulated rounding
+    ptol = dict(rtol=2e-2, atol=2.5e-1) if dtype == torch.bfloat16 else dict(rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(dga.float(), m.weight.grad.float(), **ptol)
+    torch.testing.assert_close(dba.float(), m.bias.grad.float(), **ptol)
+
+
+def test_resnet_split_grad_chain_matches_unsplit(bnmod):
+    """ResNet-50 with split-gradient block chaining vs the plain Sequential chain.  MIOpen's
+    convolutions are not bitwise reproducible run to run (atomic weight gradients), so the
+    plain chain is run twice and that noise floor bounds the split-vs-plain difference."""
+    from determined_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    model = resnet50(num_classes=10, zero_init_residual=False).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 128, 128, device="cuda").contiguous(memory_format=torch.channels_last)
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+
+    def plain(inp):
+        h = model.bn1.forward_maxpool(model.conv1(inp), model.maxpool)
+        h = model.layer4(model.layer3(model.layer2(model.layer1(h))))
+        return model.fc(torch.flatten(model.avgpool(h), 1))
+
+    def grads(fn):
+        model.load_state_dict(state)
+        model.zero_grad()
+        fn(x).float().square().mean().backward()
+        return {n: p.grad.clone() for n, p in model.named_parameters()}
+
+    ref, ref2, split = grads(plain), grads(plain), grads(model)
+    rel = lambda a, b: ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+    noise = max(rel(ref2[n], ref[n]) for n in ref)
+    worst = max(rel(split[n], ref[n]) for n in ref)
+    assert worst <= max(3 * noise, 1e-3), (worst, noise)
