@@ -70,6 +70,7 @@ void damd_bn_pool_fwd_launch(const void*, void*, uint8_t*, int64_t, int, int, in
 void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, int, int, int, int, int, const float*,
                              const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
                              hipStream_t, const void*);
+void damd_hw_broadcast_launch(const void*, void*, int64_t, int64_t, int, float, int, hipStream_t);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
                                      int, int, float, int, hipStream_t);
@@ -532,6 +533,18 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx,
   return {dx, dgamma, dbeta};
 }
 
+// backward of a global average pool over a channels-last [N, C, H, W] input: g [N, C] -> dx
+at::Tensor global_avgpool_bwd(const at::Tensor& g, int64_t H, int64_t W) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && g.size(1) % 8 == 0 &&
+              (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0, "global_avgpool_bwd: g must be a contiguous [N, C%8==0] GPU tensor");
+  TORCH_CHECK(H > 0 && W > 0, "global_avgpool_bwd: bad spatial size");
+  const int64_t N = g.size(0), C = g.size(1);
+  auto dx = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  damd_hw_broadcast_launch(g.data_ptr(), dx.data_ptr(), N, H * W, static_cast<int>(C), 1.f / static_cast<float>(H * W),
+                           dtype_code(g), cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -674,6 +687,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resid_norm_fwd", &resid_norm_fwd);
   m.def("resid_norm_bwd", &resid_norm_bwd);
   m.def("bn_pool_bwd", &bn_pool_bwd);
+  m.def("global_avgpool_bwd", &global_avgpool_bwd);
   m.doc() = "determined_amd CDNA4 HIP kernels";
   m.def("build_chunk_table", &build_chunk_table);
   m.def("chunk_entry_bytes", &chunk_entry_bytes);

@@ -773,6 +773,40 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
 }
 
 
+// ----------------------------------------------------------------------------- global avg-pool bwd
+// dx[n, h, w, c] = g[n, c] * scale over a channels-last [N, H, W, C] output (the backward of
+// x.mean((2, 3))): one vectorised write pass instead of expand + strided copy.
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+hw_broadcast_kernel(const T* __restrict__ g, T* __restrict__ out, int64_t V, int TPR, int64_t HW, float scale) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x; v < V; v += stride) {
+    const int64_t pix = v / TPR;
+    const int cg = static_cast<int>(v - pix * TPR);
+    const int64_t n = pix / HW;
+    float d[8];
+    V8<T>::ld(g + (n * TPR + cg) * 8, d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] *= scale;
+    V8<T>::st(out + v * 8, d);
+  }
+}
+
+void damd_hw_broadcast_launch(const void* g, void* out, int64_t N, int64_t HW, int C, float scale, int dtype,
+                              hipStream_t st) {
+  const int TPR = C / 8;
+  const int64_t V = N * HW * TPR;
+  const int64_t want = (V + kBNThreads - 1) / kBNThreads;
+  const dim3 grid(static_cast<unsigned>(want < 8192 ? want : 8192));
+  if (dtype == 1)
+    hipLaunchKernelGGL(hw_broadcast_kernel<bf16_t>, grid, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(g),
+                       static_cast<bf16_t*>(out), V, TPR, HW, scale);
+  else
+    hipLaunchKernelGGL(hw_broadcast_kernel<float>, grid, dim3(kBNThreads), 0, st, static_cast<const float*>(g),
+                       static_cast<float*>(out), V, TPR, HW, scale);
+  DAMD_CHECK_LAUNCH();
+}
+
 // ----------------------------------------------------------------------------- stem launchers
 // x: [N, H, W, C] (NHWC); y / idx: [N, OH, OW, C]; 3x3 / stride 2 / pad 1 pooling.
 void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, int H, int W, int C, int OH, int OW,

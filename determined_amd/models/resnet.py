@@ -12,7 +12,7 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
-from determined_amd.ops.bn import BatchNormAct2d
+from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -113,7 +113,7 @@ class ResNet(nn.Module):
         blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
         for i, blk in enumerate(blocks):
             x = blk(x, split_grad=i + 1 < len(blocks))
-        x = torch.flatten(self.avgpool(x), 1)
+        x = global_avg_pool(x)  # == flatten(self.avgpool(x), 1); fused channels-last backward
         return self.fc(x)
 
 

@@ -92,6 +92,30 @@ class _BNReLUPoolFn(torch.autograd.Function):
         return dx, dg, db, None, None, None, None, None
 
 
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """``x.mean((2, 3))`` of a channels-last activation; the backward writes the broadcast
+    gradient straight into a channels-last tensor (csrc/bn.hip ``hw_broadcast_kernel``)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        from determined_amd import ops
+
+        return ops.ext().global_avgpool_bwd(g.contiguous(), ctx.hw[0], ctx.hw[1])
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``[N, C, H, W] -> [N, C]`` mean over H, W (``flatten(AdaptiveAvgPool2d(1)(x), 1)``)."""
+    if (x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return _GlobalAvgPoolFn.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
 def _torch_bn_act(bn: nn.BatchNorm2d, x, residual, relu, momentum):
     if bn.running_mean is not None and bn.running_mean.dtype != x.dtype:
         # low-precision activations with fp32 statistics: normalise in fp32

@@ -11,5 +11,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r -o run -
 rc=$?; echo "rocprof exit $rc"; tail -2 gpurun_out/prof_r.log
 [ $rc -ne 0 ] && exit 1
 f=$(find gpurun_out/prof_r -name "*kernel_trace.csv" | head -1)
-python scripts/prof_steady.py "$f" --steps 6 --top 45 > gpurun_out/prof_r_summary.txt && cat gpurun_out/prof_r_summary.txt | head -70
+python scripts/prof_steady.py "$f" --steps 6 --top 45 --seq gpurun_out/prof_r_seq.txt > gpurun_out/prof_r_summary.txt && cat gpurun_out/prof_r_summary.txt | head -70
 rm -f "$f"

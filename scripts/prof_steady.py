@@ -17,6 +17,7 @@ ap.add_argument("trace")
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--top", type=int, default=25)
 ap.add_argument("--marker", default="damd::sgd_kernel")
+ap.add_argument("--seq", default=None, help="also write the last step's launch sequence (with grid sizes) here")
 a = ap.parse_args()
 
 rows = list(csv.DictReader(open(a.trace)))
@@ -50,3 +51,11 @@ for k, v in sorted(cats.items(), key=lambda x: -x[1][0]):
 print("top kernels (ms/step, launches/step):")
 for n, v in sorted(per.items(), key=lambda x: -x[1][0])[: a.top]:
     print(f"  {v[0]:7.3f} {v[1] / a.steps:5.0f}  {n[:110]}")
+
+if a.seq:
+    last = rows[marks[-2] + 1: marks[-1] + 1]
+    gk = [k for k in last[0].keys() if "Grid" in k or "Workgroup" in k]
+    with open(a.seq, "w") as f:
+        for r in last:
+            d = (int(r[key_end]) - int(r[key_start])) / 1e3
+            f.write(f"{d:9.1f}us  {' '.join(r[k] for k in gk):24s}  {r[name_key][:100]}\n")

@@ -190,3 +190,22 @@ def test_resnet_split_grad_chain_matches_unsplit(bnmod):
     noise = max(rel(ref2[n], ref[n]) for n in ref)
     worst = max(rel(split[n], ref[n]) for n in ref)
     assert worst <= max(3 * noise, 1e-3), (worst, noise)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_avg_pool_bwd(bnmod, dtype):
+    """channels-last global average pool: fused broadcast backward vs adaptive_avg_pool2d."""
+    from determined_amd.ops.bn import global_avg_pool
+
+    x = torch.randn(6, 2048, 7, 5, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    ya = global_avg_pool(xa)
+    yr = torch.flatten(F.adaptive_avg_pool2d(xr, 1), 1)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ya.float(), yr, **tol)
+    g = torch.randn_like(yr).to(dtype)
+    ya.backward(g)
+    yr.backward(g.float())
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, **tol)
