@@ -31,7 +31,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("DAMD_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip"]
+HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip"]
 HOST_SOURCES = ["bindings.cpp"]
 NATIVE_SOURCES = ["searcher.cpp", "scheduler.cpp", "loader.cpp", "module.cpp"]
 

@@ -66,11 +66,18 @@ void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, con
                         const float*, const float*, float*, float*, void*, void*, void*, void*, int, int, int,
                         hipStream_t, const uint8_t*, const void*);
 void damd_bn_pool_fwd_launch(const void*, void*, uint8_t*, int64_t, int, int, int, int, int, const void*, const void*,
-                             float*, float*, float, float, float*, float*, float*, float*, float*, int, int, hipStream_t);
+                             float*, float*, float, float, float*, float*, float*, float*, float*, int, int, hipStream_t,
+                             const float*, int);
 void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, int, int, int, int, int, const float*,
                              const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
                              hipStream_t, const void*);
 void damd_hw_broadcast_launch(const void*, void*, int64_t, int64_t, int, float, int, hipStream_t);
+// launchers (conv_stem.hip)
+extern "C" int damd_stem_supported(int64_t, int64_t);
+extern "C" int damd_stem_fwd_blocks(int64_t, int);
+extern "C" void damd_stem_fwd_launch(const void*, const void*, void*, float*, int64_t, int, int, hipStream_t);
+extern "C" int damd_stem_wgrad_blocks(int64_t, int);
+extern "C" void damd_stem_wgrad_launch(const void*, const void*, float*, void*, int, int64_t, int, int, hipStream_t);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
                                      int, int, float, int, hipStream_t);
@@ -473,7 +480,8 @@ std::vector<at::Tensor> resid_norm_bwd(const at::Tensor& dy, const c10::optional
 // uint8 [N*OH*OW*C], stats [4, C]).
 std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                                     const c10::optional<at::Tensor>& running_mean,
-                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps) {
+                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                                    const c10::optional<at::Tensor>& stats_part) {
   TORCH_CHECK(x.dim() == 4 && bn_supported(x), "bn_pool_fwd: need a 4-d channels-last tensor with C % 8 == 0");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
@@ -492,12 +500,22 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
   auto stats = at::empty({4, C}, fopts);
   auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto idx = at::empty({N * OH * OW * C}, x.options().dtype(at::kByte));
+  // stats_part: (sum, sum sq) partials [nb, 2, C] already produced with x (stem_conv_fwd)
+  const float* pre = nullptr;
+  int pre_nb = 0;
+  if (stats_part.has_value() && stats_part->defined()) {
+    TORCH_CHECK(stats_part->scalar_type() == at::kFloat && stats_part->dim() == 3 && stats_part->size(1) == 2 &&
+                stats_part->size(2) == C && stats_part->is_contiguous() && stats_part->device() == x.device(),
+                "bn_pool_fwd: stats_part must be a float32 [nb, 2, C] tensor");
+    pre = stats_part->data_ptr<float>();
+    pre_nb = static_cast<int>(stats_part->size(0));
+  }
   damd_bn_pool_fwd_launch(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, static_cast<int>(H), static_cast<int>(W),
                           static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW), weight.data_ptr(),
                           bias.data_ptr(), rm, rv, static_cast<float>(momentum), static_cast<float>(eps),
                           part.data_ptr<float>(), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
                           stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), dtype_code(x), dtype_code(weight),
-                          cur_stream());
+                          cur_stream(), pre, pre_nb);
   return {y, idx, stats};
 }
 
@@ -543,6 +561,48 @@ at::Tensor global_avgpool_bwd(const at::Tensor& g, int64_t H, int64_t W) {
   damd_hw_broadcast_launch(g.data_ptr(), dx.data_ptr(), N, H * W, static_cast<int>(C), 1.f / static_cast<float>(H * W),
                            dtype_code(g), cur_stream());
   return dx;
+}
+
+// ---------------------------------------------------------------- ResNet stem convolution
+// x: [N, 3, H, W] bf16 channels-last (NHWC); w: [64, 3, 7, 7]; stride 2, padding 3.
+bool stem_conv_supported(const at::Tensor& x, const at::Tensor& w) {
+  return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+         w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+         damd_stem_supported(x.size(2), x.size(3));
+}
+
+// returns (y, stats partials [nb, 2, 64] or an empty tensor) -- see conv_stem.hip
+std::vector<at::Tensor> stem_conv_fwd(const at::Tensor& x, const at::Tensor& w, bool want_stats) {
+  TORCH_CHECK(stem_conv_supported(x, w), "stem_conv_fwd: unsupported input");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  // [64][7][32] bf16 weight image: k' = 4*kw + ci with zero pad at kw = 7 / ci = 3 (28 KB)
+  auto wl = at::constant_pad_nd(w.to(at::kBFloat16).permute({0, 2, 3, 1}), {0, 1, 0, 1}).reshape({64, 7, 32}).contiguous();
+  auto y = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor part = want_stats ? at::empty({damd_stem_fwd_blocks(N, static_cast<int>(H)), 2, 64},
+                                          x.options().dtype(at::kFloat))
+                               : at::empty({0}, x.options().dtype(at::kFloat));
+  damd_stem_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr, N,
+                       static_cast<int>(H), static_cast<int>(W), cur_stream());
+  return {y, part};
+}
+
+// dW for the stem convolution, in w's dtype and memory format.
+at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& w) {
+  TORCH_CHECK(stem_conv_supported(x, w), "stem_conv_wgrad: unsupported input");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 && dy.size(2) == (H - 1) / 2 + 1 &&
+              dy.size(3) == (W - 1) / 2 + 1 && dy.scalar_type() == at::kBFloat16 &&
+              dy.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "stem_conv_wgrad: dy must be a [N, 64, OH, OW] bf16 channels-last tensor");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat, "stem_conv_wgrad: weight dtype");
+  const int nb = damd_stem_wgrad_blocks(N, static_cast<int>(H));
+  auto part = at::empty({nb, 64, 7 * 32}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({64, 3, 7, 7}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  damd_stem_wgrad_launch(x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), dtype_code(w), N,
+                         static_cast<int>(H), static_cast<int>(W), cur_stream());
+  return w.is_contiguous(at::MemoryFormat::ChannelsLast) ? dw : dw.contiguous();
 }
 
 // ---------------------------------------------------------------- flash attention
@@ -688,6 +748,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resid_norm_bwd", &resid_norm_bwd);
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("global_avgpool_bwd", &global_avgpool_bwd);
+  m.def("stem_conv_supported", &stem_conv_supported);
+  m.def("stem_conv_fwd", &stem_conv_fwd);
+  m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.doc() = "determined_amd CDNA4 HIP kernels";
   m.def("build_chunk_table", &build_chunk_table);
   m.def("chunk_entry_bytes", &chunk_entry_bytes);

@@ -181,7 +181,9 @@ bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, int
   float s, ss;
   reduce_partials(part, nb, C, c, q, s, ss);
   if (q == 0 && c < C) {
-    const float K = x_is_bf16 ? bf2f(static_cast<const bf16_t*>(xbase)[c]) : static_cast<const float*>(xbase)[c];
+    // pilot: row 0 of x (bn_stats_kernel), or 0 for producer-computed plain sums (xbase null)
+    const float K = xbase == nullptr ? 0.f
+                    : x_is_bf16 ? bf2f(static_cast<const bf16_t*>(xbase)[c]) : static_cast<const float*>(xbase)[c];
     const float n = static_cast<float>(M);
     const float dm = s / n;
     const float var = fmaxf(ss / n - dm * dm, 0.f);
@@ -812,20 +814,26 @@ void damd_hw_broadcast_launch(const void* g, void* out, int64_t N, int64_t HW, i
 void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, int H, int W, int C, int OH, int OW,
                              const void* w, const void* b, float* run_mean, float* run_var, float momentum, float eps,
                              float* part, float* mean, float* invstd, float* scale, float* shift, int x_dtype,
-                             int w_dtype, hipStream_t st) {
+                             int w_dtype, hipStream_t st, const float* pre_part, int pre_nb) {
   const int64_t M = N * H * W;
   int nb;
-  const int64_t rpb = rows_per_block_for(M, C, &nb);
-  if (x_dtype == 1)
+  int64_t rpb = rows_per_block_for(M, C, &nb);
+  const void* pilot = x;
+  if (pre_part != nullptr) {  // plain (sum, sum sq) partials from the producing kernel
+    part = const_cast<float*>(pre_part);
+    nb = pre_nb;
+    pilot = nullptr;
+  } else if (x_dtype == 1) {
     hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
-  else
+  } else {
     hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+  }
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
   const int TPR = C / 8;
   const int64_t Vout = N * OH * OW * TPR;

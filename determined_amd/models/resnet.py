@@ -13,6 +13,8 @@ import torch
 from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
+from determined_amd.ops import fusion_enabled
+from determined_amd.ops.conv import stem_conv2d
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -109,10 +111,13 @@ class ResNet(nn.Module):
         # Every activation between blocks feeds two consumers (next conv1 + shortcut): producers
         # hand out split-gradient pairs so the backward sums the two gradients inside the BN
         # kernels instead of in separate elementwise adds (ops/bn.py).
-        x = self.bn1.forward_maxpool(self.conv1(x), self.maxpool, split_grad=True)
+        # stem conv emits the BN batch-statistic partials from its epilogue (ops/conv.py)
+        split = fusion_enabled("split_grad")
+        y, part = stem_conv2d(self.conv1, x, with_stats=True)
+        x = self.bn1.forward_maxpool(y, self.maxpool, split_grad=split, stats_part=part)
         blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
         for i, blk in enumerate(blocks):
-            x = blk(x, split_grad=i + 1 < len(blocks))
+            x = blk(x, split_grad=split and i + 1 < len(blocks))
         x = global_avg_pool(x)  # == flatten(self.avgpool(x), 1); fused channels-last backward
         return self.fc(x)
 

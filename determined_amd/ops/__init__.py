@@ -50,6 +50,16 @@ def ext() -> Any:
     return e
 
 
+_DISABLED = frozenset(f.strip() for f in os.environ.get("DAMD_DISABLE_FUSIONS", "").split(",") if f.strip())
+
+
+def fusion_enabled(name: str) -> bool:
+    """Model-level fusions can be switched off for A/B measurements with
+    ``DAMD_DISABLE_FUSIONS=stem_conv,stem_stats,split_grad,avgpool`` (the replacement is the
+    plain PyTorch / MIOpen composition, never a silent eager fallback of a kernel)."""
+    return name not in _DISABLED
+
+
 from determined_amd.ops.optim import FusedAdamW, FusedSGD, fused_clip_grad_norm_  # noqa: E402
 from determined_amd.ops.norm import (  # noqa: E402
     FusedLayerNorm,

@@ -70,10 +70,11 @@ class _BNReLUPoolFn(torch.autograd.Function):
     two BN-backward passes."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, split=False):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, split=False, stats_part=None):
         from determined_amd import ops
 
-        y, idx, stats = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum), float(eps))
+        y, idx, stats = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum), float(eps),
+                                              stats_part)
         ctx.save_for_backward(x, idx, stats, weight)
         ctx.mark_non_differentiable(idx)
         if split:
@@ -87,9 +88,9 @@ class _BNReLUPoolFn(torch.autograd.Function):
         x, idx, stats, weight = ctx.saved_tensors
         dy, dy2 = _sum_grads(dy, dy2, torch.channels_last)
         if dy is None:
-            return (None,) * 8
+            return (None,) * 9
         dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight, dy2)
-        return dx, dg, db, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None
 
 
 class _GlobalAvgPoolFn(torch.autograd.Function):
@@ -110,8 +111,10 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
 
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """``[N, C, H, W] -> [N, C]`` mean over H, W (``flatten(AdaptiveAvgPool2d(1)(x), 1)``)."""
+    from determined_amd import ops
+
     if (x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32)
-            and x.is_contiguous(memory_format=torch.channels_last)):
+            and x.is_contiguous(memory_format=torch.channels_last) and ops.fusion_enabled("avgpool")):
         return _GlobalAvgPoolFn.apply(x)
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
@@ -193,7 +196,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return F.relu(y) if self.act else y
         return e.bn_apply(x, scale, shift, residual, self.act)
 
-    def forward_maxpool(self, x: torch.Tensor, pool: nn.MaxPool2d, split_grad: bool = False):
+    def forward_maxpool(self, x: torch.Tensor, pool: nn.MaxPool2d, split_grad: bool = False,
+                        stats_part: Optional[torch.Tensor] = None):
         """``pool(self(x))`` with the fused stem kernels when ``pool`` is the ResNet 3x3/s2/p1
         max-pool, training mode and a supported channels-last GPU tensor; exact composition
         otherwise."""
@@ -212,8 +216,9 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self._nbt_host = self._nbt() + 1
         if self.momentum is None:
             momentum = 1.0 / float(self._nbt_host)
+        # stats_part: batch-statistic partials the producer of x already computed (ops/conv.py)
         return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, momentum, self.eps,
-                                   split_grad)
+                                   split_grad, stats_part)
 
     def _apply(self, fn, recurse: bool = True):
         # Running statistics always stay fp32 (a bf16 running_var loses the update signal).

@@ -237,3 +237,49 @@ def test_residual_dropout_layernorm_fused(dtype, H):
     torch.testing.assert_close(s2.float()[kept], torch.full_like(s2.float()[kept], 1 / (1 - p)), rtol=1e-2, atol=1e-2)
     s2.backward(torch.ones_like(s2))
     torch.testing.assert_close(b2.grad.float(), kept.float() / (1 - p), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64), (3, 32, 96), (2, 224, 224)])
+@pytest.mark.parametrize("wdtype", [torch.bfloat16, torch.float32])
+def test_stem_conv_matches_reference(shape, wdtype):
+    """csrc/conv_stem.hip forward + weight gradient vs an fp32 PyTorch conv of the same bf16 data."""
+    from determined_amd.ops.conv import stem_conv2d, stem_fusable
+
+    torch.manual_seed(0)
+    N, H, W = shape
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().to(wdtype)
+    x = torch.randn(N, 3, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert stem_fusable(conv, x)
+    y = stem_conv2d(conv, x)
+    xr = x.float()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, stride=2, padding=3)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    dw = conv.weight.grad
+    assert dw.dtype == wdtype and dw.shape == wr.shape
+    rel = ((dw.float() - wr.grad).norm() / wr.grad.norm()).item()
+    assert rel < 1e-2, rel
+
+
+def test_stem_conv_bn_stats_fusion():
+    """Stem conv epilogue statistics feed the fused BN+ReLU+MaxPool: same result as the BN
+    computing its own statistics."""
+    import determined_amd.ops as ops
+    from determined_amd.ops.conv import stem_conv2d
+
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().to(torch.bfloat16)
+    bn_a, bn_b = ops.BatchNormAct2d(64).cuda(), ops.BatchNormAct2d(64).cuda()
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = (torch.randn(4, 3, 96, 96, device="cuda") + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y, part = stem_conv2d(conv, x, with_stats=True)
+    assert part is not None and part.shape[1:] == (2, 64)
+    out_a = bn_a.forward_maxpool(y, pool, stats_part=part)
+    out_b = bn_b.forward_maxpool(y.detach(), pool)
+    torch.testing.assert_close(out_a.float(), out_b.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-4)
