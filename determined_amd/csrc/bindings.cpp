@@ -91,6 +91,8 @@ extern "C" void damd_lm_ce_bwd_launch(const void*, const int64_t*, const float*,
                                       int, int64_t, void*, hipStream_t);
 extern "C" int damd_bias_grad_splits(int64_t, int);
 extern "C" void damd_bias_grad_launch(const void*, int64_t, int, int, float*, void*, int, hipStream_t);
+extern "C" void damd_gelu_fwd_launch(const void*, void*, int64_t, hipStream_t);
+extern "C" void damd_gelu_bwd_bias_launch(const void*, const void*, void*, int64_t, int, int, float*, hipStream_t);
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -729,12 +731,41 @@ at::Tensor bias_grad(const at::Tensor& g, at::ScalarType out_dtype) {
   return out;
 }
 
+// gelu (tanh approximation) of a contiguous bf16 tensor (numel % 8 == 0)
+at::Tensor gelu_fwd(const at::Tensor& h) {
+  TORCH_CHECK(h.is_cuda() && h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.numel() % 8 == 0 &&
+              (reinterpret_cast<uintptr_t>(h.data_ptr()) & 15) == 0, "gelu_fwd: contiguous bf16 GPU tensor, numel % 8 == 0");
+  auto g = at::empty_like(h);
+  damd_gelu_fwd_launch(h.data_ptr(), g.data_ptr(), h.numel(), cur_stream());
+  return g;
+}
+
+// (dh, dbias) for g = gelu(h), h = x W^T + b: dh = gelu'(h) * dg and dbias = column sums of dh
+std::vector<at::Tensor> gelu_bwd_bias(const at::Tensor& dg, const at::Tensor& h, at::ScalarType bias_dtype) {
+  TORCH_CHECK(dg.is_cuda() && dg.scalar_type() == at::kBFloat16 && dg.is_contiguous() && h.is_contiguous() &&
+              h.scalar_type() == at::kBFloat16 && dg.sizes() == h.sizes(), "gelu_bwd_bias: matching contiguous bf16 tensors");
+  const int64_t N = h.size(-1), M = h.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(N % 8 == 0, "gelu_bwd_bias needs N % 8 == 0");
+  TORCH_CHECK(bias_dtype == at::kFloat || bias_dtype == at::kBFloat16, "bias dtype f32/bf16");
+  auto dh = at::empty_like(h);
+  auto db = at::empty({N}, h.options().dtype(bias_dtype));
+  const int splits = damd_bias_grad_splits(M, static_cast<int>(N));
+  auto part = at::empty({splits, N}, h.options().dtype(at::kFloat));
+  damd_gelu_bwd_bias_launch(dg.data_ptr(), h.data_ptr(), dh.data_ptr(), M, static_cast<int>(N), splits,
+                            part.data_ptr<float>(), cur_stream());
+  damd_norm_wgrad_finalize_launch(part.data_ptr<float>(), nullptr, splits, static_cast<int>(N), db.data_ptr(),
+                                  nullptr, bias_dtype == at::kFloat ? 0 : 1, cur_stream());
+  return {dh, db};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lm_ce_fwd", &lm_ce_fwd);
   m.def("lm_ce_bwd", &lm_ce_bwd);
   m.def("bias_grad", &bias_grad);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd_bias", &gelu_bwd_bias);
   m.def("attn_supported", &attn_supported);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -12,6 +12,11 @@
 //
 // bias_grad: column sums of a [M, N] bf16 gradient (the bias gradient of a Linear) with
 //   16-byte loads into row-split fp32 partials; the wide finalize of norm.hip finishes them.
+//
+// gelu (tanh approximation) after a Linear (GPT-2 MLP): forward g = gelu(h) as one vectorised
+//   pass; backward dh = gelu'(h) * dg FUSED with the bias gradient of that Linear -- the
+//   column partials of dh are accumulated while dh is written, so dh is never re-read for
+//   the bias (replaces torch's GeluBackward + a separate column-sum pass).
 
 #include "common.h"
 
@@ -150,6 +155,69 @@ bias_grad_partial_kernel(const bf16_t* __restrict__ g, int64_t M, int N, int64_t
   }
 }
 
+constexpr float kGeluC = 0.7978845608028654f;  // sqrt(2 / pi)
+constexpr float kGeluA = 0.044715f;
+
+__device__ __forceinline__ float tanh_fast(float u) {
+  // 1 - 2 / (exp(2u) + 1): exact limits at +-inf, fp32 accuracy well below bf16 rounding
+  return 1.f - 2.f / (__expf(2.f * u) + 1.f);
+}
+
+__global__ void __launch_bounds__(256)
+gelu_fwd_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ g, int64_t nvec) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < nvec; i += stride) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(h + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = bf2f(v.v[j]);
+      const float t = tanh_fast(kGeluC * (x + kGeluA * x * x * x));
+      o.v[j] = f2bf(0.5f * x * (1.f + t));
+    }
+    *reinterpret_cast<bf16x8*>(g + i * 8) = o;
+  }
+}
+
+// dh = gelu'(h) * dg (bf16 out) + fp32 column partials of dh: part[blockIdx.y][N]
+__global__ void __launch_bounds__(256)
+gelu_bwd_bias_kernel(const bf16_t* __restrict__ dg, const bf16_t* __restrict__ h, bf16_t* __restrict__ dh, int64_t M,
+                     int N, int64_t rows_per_split, float* __restrict__ part) {
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * kBGCols + cl * 8;
+  const int64_t r0 = blockIdx.y * rows_per_split;
+  const int64_t r1 = min(M, r0 + rows_per_split);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+    for (int64_t r = r0 + rl; r < r1; r += kBGRowLanes) {
+      const int64_t off = r * N + col;
+      const bf16x8 d = *reinterpret_cast<const bf16x8*>(dg + off);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(h + off);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = bf2f(v.v[j]);
+        const float t = tanh_fast(kGeluC * (x + kGeluA * x * x * x));
+        const float dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluC * (1.f + 3.f * kGeluA * x * x);
+        o.v[j] = f2bf(dgelu * bf2f(d.v[j]));
+        acc[j] += bf2f(o.v[j]);  // the bias gradient sums the bf16 dh the weight GEMMs see
+      }
+      *reinterpret_cast<bf16x8*>(dh + off) = o;
+    }
+  }
+  __shared__ float red[kBGRowLanes][kBGCols + 4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cl * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < kBGCols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kBGRowLanes; ++k) s += red[k][threadIdx.x];
+    const int gc = blockIdx.x * kBGCols + threadIdx.x;
+    if (gc < N) part[static_cast<int64_t>(blockIdx.y) * N + gc] = s;
+  }
+}
+
 }  // namespace fused
 }  // namespace damd
 
@@ -192,6 +260,26 @@ void damd_bias_grad_launch(const void* g, int64_t M, int N, int splits, float* p
   const int64_t rps = (M + splits - 1) / splits;
   dim3 grid((N + kBGCols - 1) / kBGCols, splits);
   hipLaunchKernelGGL(bias_grad_partial_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g), M, N, rps, part);
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_gelu_fwd_launch(const void* h, void* g, int64_t n, hipStream_t st) {
+  const int64_t nvec = n / 8;
+  if (nvec <= 0) return;
+  const int64_t want = (nvec + 255) / 256;
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(static_cast<unsigned>(want < 8192 ? want : 8192)), dim3(256), 0, st,
+                     static_cast<const bf16_t*>(h), static_cast<bf16_t*>(g), nvec);
+  DAMD_CHECK_LAUNCH();
+}
+
+// dh and bias-gradient partials [splits, N] (splits from damd_bias_grad_splits)
+void damd_gelu_bwd_bias_launch(const void* dg, const void* h, void* dh, int64_t M, int N, int splits, float* part,
+                               hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  const int64_t rps = (M + splits - 1) / splits;
+  dim3 grid((N + kBGCols - 1) / kBGCols, splits);
+  hipLaunchKernelGGL(gelu_bwd_bias_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(dg),
+                     static_cast<const bf16_t*>(h), static_cast<bf16_t*>(dh), M, N, rps, part);
   DAMD_CHECK_LAUNCH();
 }
 

@@ -28,7 +28,7 @@ from torch import nn
 from torch.utils.checkpoint import checkpoint
 
 from determined_amd.ops.attention import qkv_attention
-from determined_amd.ops.fused import FusedLinear, lm_cross_entropy
+from determined_amd.ops.fused import FusedLinear, linear_gelu, lm_cross_entropy
 from determined_amd.ops.norm import FusedLayerNorm
 
 
@@ -88,7 +88,7 @@ class MLP(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x: torch.Tensor, residual_dropout: bool = True) -> torch.Tensor:
-        out = self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+        out = self.c_proj(linear_gelu(self.c_fc, x))  # bias + GELU fused (ops/fused.py)
         return self.drop(out) if residual_dropout else out
 
 
@@ -138,8 +138,12 @@ class GPT2LMHeadModel(nn.Module):
             nn.init.normal_(m.weight, mean=0.0, std=0.02)
 
     def zero3_external_parameters(self):
-        """ZeRO-3: the tied LM head reads ``wte.weight`` in this module's forward."""
-        return [(self, self.wte.weight)]
+        """ZeRO-3: the tied LM head reads ``wte.weight`` in this module's forward, and each MLP
+        reads its ``c_fc`` parameters directly (fused bias + GELU, ops/fused.py linear_gelu)."""
+        ext = [(self, self.wte.weight)]
+        for blk in self.h:
+            ext += [(blk.mlp, blk.mlp.c_fc.weight), (blk.mlp, blk.mlp.c_fc.bias)]
+        return ext
 
     def num_parameters(self, exclude_embeddings: bool = False) -> int:
         n = sum(p.numel() for p in self.parameters())

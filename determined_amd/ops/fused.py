@@ -76,6 +76,35 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class _LinearGeluFn(torch.autograd.Function):
+    """``gelu_tanh(x W^T + b)``: the GEMM (bias in the hipBLASLt epilogue) plus one GELU pass
+    forward; backward fuses gelu' with the bias gradient (csrc/fused.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        h = F.linear(x, weight, bias)
+        ctx.save_for_backward(x, weight, h)
+        return _ext().gelu_fwd(h)
+
+    @staticmethod
+    def backward(ctx, dg):
+        x, weight, h = ctx.saved_tensors
+        dh, db = _ext().gelu_bwd_bias(dg.contiguous(), h, weight.dtype)
+        dh2 = dh.view(-1, dh.shape[-1])
+        dx = (dh2 @ weight).view(*dh.shape[:-1], weight.shape[1]) if ctx.needs_input_grad[0] else None
+        dw = dh2.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        return dx, dw, (db if ctx.needs_input_grad[2] else None)
+
+
+def linear_gelu(linear: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """``F.gelu(linear(x), approximate="tanh")`` with the fused HIP GELU kernels on bf16 GPU
+    tensors; the plain composition elsewhere."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and linear.bias is not None and linear.out_features % 8 == 0 \
+            and linear.weight.dtype == torch.bfloat16 and x.is_contiguous():
+        return _LinearGeluFn.apply(x, linear.weight, linear.bias)
+    return F.gelu(linear(x), approximate="tanh")
+
+
 class FusedLinear(nn.Linear):
     """``nn.Linear`` with a single-pass bf16 bias-gradient kernel on the GPU."""
 

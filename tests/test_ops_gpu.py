@@ -283,3 +283,24 @@ def test_stem_conv_bn_stats_fusion():
     torch.testing.assert_close(out_a.float(), out_b.float(), rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-4)
+
+
+def test_linear_gelu_fused_matches_reference():
+    """Fused GELU forward / GELU'+bias-gradient backward vs the fp32 PyTorch composition."""
+    from determined_amd.ops.fused import linear_gelu
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 1024).cuda().to(torch.bfloat16)
+    x = torch.randn(3, 77, 256, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = linear_gelu(lin, x)
+    xr = x.detach().float().requires_grad_(True)
+    wr = lin.weight.detach().float().requires_grad_(True)
+    br = lin.bias.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.gelu(torch.nn.functional.linear(xr, wr, br), approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    for got, ref in ((x.grad, xr.grad), (lin.weight.grad, wr.grad), (lin.bias.grad, br.grad)):
+        rel = ((got.float() - ref).norm() / ref.norm()).item()
+        assert rel < 1e-2, rel
