@@ -28,13 +28,23 @@ def main() -> None:
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
     ap.add_argument("--bucket", type=int, default=16 * 1024 * 1024)
-    ap.add_argument("--tunable", default="", help="enable PyTorch TunableOp GEMM tuning; results file path")
+    default_tun = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop", "gpt2_345m_mb8.csv")
+    # in-tree TunableOp choices (+1% same-box at mb 8; shapes not in the file keep hipBLASLt's
+    # default); --tunable "" disables
+    ap.add_argument("--tunable", default=default_tun if os.path.exists(default_tun) else "",
+                    help="PyTorch TunableOp GEMM results file (use it)")
+    ap.add_argument("--tune", action="store_true", help="with --tunable: search and (re)write the file")
     a = ap.parse_args()
     if a.tunable:
-        # hipBLASLt/rocBLAS solution search per GEMM shape (done during warm-up, cached in a file)
+        # hipBLASLt/rocBLAS solution choice per GEMM shape from a results file; --tune searches
+        # during warm-up (bounded per solution) and writes the file at the end
         torch.cuda.tunable.enable(True)
-        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.tuning_enable(a.tune)
+        torch.cuda.tunable.set_max_tuning_duration(20)
+        torch.cuda.tunable.set_max_tuning_iterations(20)
         torch.cuda.tunable.set_filename(a.tunable)
+        if not a.tune:
+            torch.cuda.tunable.read_file(a.tunable)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
