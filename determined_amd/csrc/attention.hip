@@ -74,7 +74,18 @@ __device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
 }
 
-__device__ __forceinline__ short bfs(float x) { return static_cast<short>(f2bf(x)); }
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef short sh2 __attribute__((ext_vector_type(2)));
+
+// gfx950 converts fp32 -> bf16 (round to nearest even) in hardware: one v_cvt_pk_bf16_f32 per
+// pair instead of the ~6-instruction software rounding (the kernels are VALU-bound, not MFMA).
+__device__ __forceinline__ sh2 cvt2(float a, float b) {
+  return __builtin_bit_cast(sh2, __builtin_convertvector((f2{a, b}), bf2));
+}
+__device__ __forceinline__ short bfs(float x) { return cvt2(x, 0.f)[0]; }
+// raw v_exp_f32 (softmax arguments are <= 0 or -inf; no denormal-range fixup needed)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ s8 cat4(s4 lo, s4 hi) {
   s8 r;
@@ -85,9 +96,10 @@ __device__ __forceinline__ s8 cat4(s4 lo, s4 hi) {
 
 // bf16 fragment from two 16-wide accumulator tiles (the permuted 32-wide k step).
 __device__ __forceinline__ s8 pack_pair(f4 lo, f4 hi) {
+  const sh2 a = cvt2(lo[0], lo[1]), b = cvt2(lo[2], lo[3]), c = cvt2(hi[0], hi[1]), d = cvt2(hi[2], hi[3]);
   s8 r;
-  r[0] = bfs(lo[0]); r[1] = bfs(lo[1]); r[2] = bfs(lo[2]); r[3] = bfs(lo[3]);
-  r[4] = bfs(hi[0]); r[5] = bfs(hi[1]); r[6] = bfs(hi[2]); r[7] = bfs(hi[3]);
+  r[0] = a[0]; r[1] = a[1]; r[2] = b[0]; r[3] = b[1];
+  r[4] = c[0]; r[5] = c[1]; r[6] = d[0]; r[7] = d[1];
   return r;
 }
 
@@ -199,31 +211,30 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int qt = 0; qt < kQT; ++qt) {
       const int myq = qw + qt * 16 + c;
+      // raw scores; the softmax scale (> 0) is folded into the exp2 argument: p = 2^(s*c - m)
       float mx = -INFINITY;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = s[qt][nt][r] * a.scale_log2;
           if (need_mask) {
             const int key = k0 + nt * 16 + 4 * g + r;
-            if (key >= T || (CAUSAL && key > myq)) v = -INFINITY;
+            if (key >= T || (CAUSAL && key > myq)) s[qt][nt][r] = -INFINITY;
           }
-          s[qt][nt][r] = v;
-          mx = fmaxf(mx, v);
+          mx = fmaxf(mx, s[qt][nt][r]);
         }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m[qt], mx);
+      const float m_new = fmaxf(m[qt], mx * a.scale_log2);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m[qt] - m_use);
+      const float alpha = ex2(m[qt] - m_use);
       float rs = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[qt][nt][r] - m_use);
+          const float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -m_use));
           s[qt][nt][r] = p;
           rs += p;
         }
@@ -362,7 +373,7 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = qt * 16 + 4 * g + r;
-        float p = exp2f(sacc[r] * a.scale_log2 - lse2[ql]);
+        float p = ex2(fmaf(sacc[r], a.scale_log2, -lse2[ql]));
         if (need_mask && (mykey >= T || (CAUSAL && mykey > q0 + ql))) p = 0.f;
         P[qt][r] = p;
         dS[qt][r] = p * (dpacc[r] - dl[ql]);
@@ -487,7 +498,7 @@ __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
       for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = exp2f(s[qt][nt][r] * a.scale_log2 - lse2[qt]);
+          float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -lse2[qt]));
           if (need_mask) {
             const int key = k0 + nt * 16 + 4 * g + r;
             if (key >= T || (CAUSAL && key > myq)) p = 0.f;
