@@ -32,6 +32,14 @@ CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("DAMD_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip"]
+# MFMA kernels whose accumulators are also touched by VALU code (online softmax, rescales):
+# keep them in the unified VGPR file instead of AGPRs, which otherwise costs a
+# v_accvgpr_read/write pair per element per tile (attention: 450 copies per kv tile) and
+# lowers occupancy.
+HIP_EXTRA_FLAGS = {
+    "attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    "conv_stem.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
 HOST_SOURCES = ["bindings.cpp"]
 NATIVE_SOURCES = ["searcher.cpp", "scheduler.cpp", "loader.cpp", "module.cpp"]
 
@@ -86,7 +94,8 @@ def build_hip_ops(force: bool = False, jobs: int = 8) -> pathlib.Path:
         o = BUILD / (src + ".o")
         objs.append(o)
         if force or _newer(o, [s] + headers):
-            jobs_list.append([HIPCC, *common, "-munsafe-fp-atomics", "-c", str(s), "-o", str(o)])
+            jobs_list.append([HIPCC, *common, "-munsafe-fp-atomics", *HIP_EXTRA_FLAGS.get(src, []), "-c", str(s),
+                              "-o", str(o)])
     for src in HOST_SOURCES:
         s = csrc / src
         o = BUILD / (src + ".o")
