@@ -35,6 +35,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace damd {
 namespace attn {
 
@@ -183,7 +185,12 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
   Stage<D, kBlk> ks, vs;
   ks.load(Kp, a.sk.t, 0, T);
   vs.load(Vp, a.sv.t, 0, T);
-  for (int kb = 0; kb < kb_end; ++kb) {
+  // Leading tiles that no row of the workgroup masks (all keys < T and <= q0) run a body
+  // compiled without any masking code; only the <= 2 diagonal / ragged tiles carry the selects.
+  // (D = 128: a single masked body -- the unmasked copy pushes it to 256 VGPRs, 1 wave / SIMD)
+  const int kb_full = D == 64 ? min(kb_end, CAUSAL ? min((q0 + 1) / kBlk, T / kBlk) : T / kBlk) : 0;
+  auto tile = [&](int kb, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
     const int k0 = kb * kBlk;
     __syncthreads();
     ks.store(Ks);
@@ -207,23 +214,23 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
         for (int qt = 0; qt < kQT; ++qt) s[qt][nt] = mfma(kf, qf[qt][ds], s[qt][nt]);
       }
     }
-    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && k0 + kBlk - 1 > qw);
 #pragma unroll
     for (int qt = 0; qt < kQT; ++qt) {
       const int myq = qw + qt * 16 + c;
       // raw scores; the softmax scale (> 0) is folded into the exp2 argument: p = 2^(s*c - m)
+      if constexpr (MASK) {
+        const int kmax = CAUSAL ? min(T - 1, myq) : T - 1;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            s[qt][nt][r] = (k0 + nt * 16 + 4 * g + r > kmax) ? -INFINITY : s[qt][nt][r];
+      }
       float mx = -INFINITY;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (need_mask) {
-            const int key = k0 + nt * 16 + 4 * g + r;
-            if (key >= T || (CAUSAL && key > myq)) s[qt][nt][r] = -INFINITY;
-          }
-          mx = fmaxf(mx, s[qt][nt][r]);
-        }
-      }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qt][nt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m[qt], mx * a.scale_log2);
@@ -256,7 +263,10 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
         for (int qt = 0; qt < kQT; ++qt) oacc[qt][dt] = mfma(vf, pb[qt], oacc[qt][dt]);
       }
     }
-  }
+  };
+  int kb = 0;
+  for (; kb < kb_full; ++kb) tile(kb, std::false_type{});
+  for (; kb < kb_end; ++kb) tile(kb, std::true_type{});
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     float lt = l[qt];
@@ -374,7 +384,7 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int ql = qt * 16 + 4 * g + r;
         float p = ex2(fmaf(sacc[r], a.scale_log2, -lse2[ql]));
-        if (need_mask && (mykey >= T || (CAUSAL && mykey > q0 + ql))) p = 0.f;
+        if (need_mask) p = (mykey >= T || (CAUSAL && mykey > q0 + ql)) ? 0.f : p;
         P[qt][r] = p;
         dS[qt][r] = p * (dpacc[r] - dl[ql]);
       }
@@ -494,15 +504,13 @@ __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
 #pragma unroll
     for (int qt = 0; qt < kQT; ++qt) {
       const int myq = qw + qt * 16 + c;
+      const int kmax = CAUSAL ? min(T - 1, myq) : T - 1;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -lse2[qt]));
-          if (need_mask) {
-            const int key = k0 + nt * 16 + 4 * g + r;
-            if (key >= T || (CAUSAL && key > myq)) p = 0.f;
-          }
+          if (need_mask) p = (k0 + nt * 16 + 4 * g + r > kmax) ? 0.f : p;
           s[qt][nt][r] = p * (dp[qt][nt][r] - dl[qt]);  // dS^T
         }
       }
