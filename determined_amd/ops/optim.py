@@ -211,10 +211,22 @@ class _FusedBase(torch.optim.Optimizer):
         from determined_amd import ops
 
         e = ops.ext()
-        buckets = self._gpu_buckets()
-        by_dev: Dict[torch.device, List[Tuple[Any, _Plan]]] = {}
-        for key, b in buckets.items():
-            by_dev.setdefault(key[0], []).append((key, self._plan_for(key, b)))
+        # Host fast path: rebuilding the buckets/plans walks every parameter in Python (~10 us
+        # each; ~1.4 ms per step for the 145 ZeRO fragments of GPT-2 345M, during which the GPU
+        # sat idle).  Gradients are persistent bucket views, so a signature of the parameter /
+        # gradient objects and their storage identifies a step whose plans are unchanged.
+        # Stored in ``_plans``: every ``_plans.clear()`` (checkpoint load, re-shard) drops it.
+        sig = tuple((id(p), id(p.grad), p.grad.data_ptr()) if p.grad is not None else (id(p),)
+                    for g in self.param_groups for p in g["params"])
+        fast = self._plans.get("__fast__")
+        if fast is not None and fast[0] == sig:
+            by_dev = fast[1]
+        else:
+            buckets = self._gpu_buckets()
+            by_dev = {}
+            for key, b in buckets.items():
+                by_dev.setdefault(key[0], []).append((key, self._plan_for(key, b)))
+            self._plans["__fast__"] = (sig, by_dev)
         for dev, plans in by_dev.items():
             step_t = self._step_tensor(dev)
             need_norm = self.max_grad_norm is not None or check_finite

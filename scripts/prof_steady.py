@@ -56,6 +56,9 @@ if a.seq:
     last = rows[marks[-2] + 1: marks[-1] + 1]
     gk = [k for k in last[0].keys() if "Grid" in k or "Workgroup" in k]
     with open(a.seq, "w") as f:
+        prev_end = None
         for r in last:
             d = (int(r[key_end]) - int(r[key_start])) / 1e3
-            f.write(f"{d:9.1f}us  {' '.join(r[k] for k in gk):24s}  {r[name_key][:100]}\n")
+            gap = 0.0 if prev_end is None else (int(r[key_start]) - prev_end) / 1e3
+            prev_end = max(prev_end or 0, int(r[key_end]))
+            f.write(f"{d:9.1f}us gap {gap:7.1f}us  {' '.join(r[k] for k in gk):24s}  {r[name_key][:100]}\n")
