@@ -51,6 +51,11 @@ constexpr int kThreads = 256;  // 4 waves
 constexpr int kQT = 2;         // 16-row query tiles per wave in the forward
 constexpr int kFwdRows = 4 * 16 * kQT;
 constexpr float kLog2e = 1.4426950408889634f;
+// LDS row stride of the staged K/V/Q/dO tiles: D + 16 elements makes both the row-major
+// ds_read_b128 operand reads (lane groups {0-3,12-15,20-27}, ...) and the transposed
+// ds_read_b64_tr_b16 reads (2 x 32 lanes) bank-conflict-free; D + 8 was 2-way on both
+// (SQ_LDS_BANK_CONFLICT ~40% of LDS cycles).
+constexpr int kLdsStride(int D) { return D + 16; }
 constexpr float kLn2 = 0.6931471805599453f;
 
 struct Strides {
@@ -119,7 +124,7 @@ __device__ __forceinline__ s8 tr_pair(const bf16_t* img, int stride, int r0, int
 }
 
 // Register-staged tile of `ROWS` x D bf16: global -> registers (issued early), registers ->
-// row-major LDS image (row stride D + 8).  Rows >= T load zeros.
+// row-major LDS image (row stride kLdsStride(D)).  Rows >= T load zeros.
 template <int D, int ROWS>
 struct Stage {
   static constexpr int CH = D / 8;
@@ -138,7 +143,7 @@ struct Stage {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int idx = threadIdx.x + i * kThreads, row = idx / CH, col = (idx % CH) * 8;
-      *reinterpret_cast<s8*>(img + row * (D + 8) + col) = r[i];
+      *reinterpret_cast<s8*>(img + row * kLdsStride(D) + col) = r[i];
     }
   }
 };
@@ -148,7 +153,7 @@ struct Stage {
 // ------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
-  constexpr int KP = D + 8;
+  constexpr int KP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[kBlk * KP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
@@ -317,7 +322,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
-  constexpr int RP = D + 8;
+  constexpr int RP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[kBlk * RP];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[kBlk * RP];
   __shared__ float lse2[kBlk], dl[kBlk];
@@ -429,7 +434,7 @@ struct DqArgs {
 // dQ for a block of kFwdRows query rows (same wave / lane layout as the forward).
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
-  constexpr int KP = D + 8;
+  constexpr int KP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[kBlk * KP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
