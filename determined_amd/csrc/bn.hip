@@ -35,7 +35,11 @@ template <> struct V8<bf16_t> {
   static __device__ __forceinline__ void st(bf16_t* p, const float* o) {
     bf16x8 r;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) r.v[k] = f2bf(o[k]);
+    for (int k = 0; k < 8; k += 2) {
+      const u16v2_t q = f2bf2(o[k], o[k + 1]);
+      r.v[k] = q[0];
+      r.v[k + 1] = q[1];
+    }
     *reinterpret_cast<bf16x8*>(p) = r;
   }
 };

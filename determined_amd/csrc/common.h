@@ -21,13 +21,16 @@ __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(static_cast<uint32_t>(x) << 16);
 }
 
-// round-to-nearest-even fp32 -> bf16 (NaN preserved as quiet NaN)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+typedef __bf16 bf16v2_t __attribute__((ext_vector_type(2)));
+typedef float f32v2_t __attribute__((ext_vector_type(2)));
+typedef uint16_t u16v2_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even fp32 -> bf16 (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32, one
+// instruction per PAIR, instead of the 6-instruction integer rounding sequence.
+__device__ __forceinline__ u16v2_t f2bf2(float a, float b) {
+  return __builtin_bit_cast(u16v2_t, __builtin_convertvector((f32v2_t{a, b}), bf16v2_t));
 }
+__device__ __forceinline__ bf16_t f2bf(float f) { return f2bf2(f, 0.f)[0]; }
 
 // Scalar load/store of either float or bf16 storage as float.
 template <typename T> struct Elem;
