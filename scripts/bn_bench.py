@@ -50,3 +50,11 @@ for H, C, res in SHAPES:
                       "fwd_GBps": round(pf * nbytes / tf / 1e6), "bwd_GBps": round(pb * nbytes / tb / 1e6)}),
           flush=True)
 print(json.dumps({k: round(v, 3) for k, v in tot.items()}))
+# ceiling references on the same box: device copy (1R + 1W) and an elementwise add (2R + 1W)
+big = torch.randn(512 * 56 * 56 * 256, device="cuda", dtype=torch.bfloat16)
+big2 = torch.randn_like(big)
+out = torch.empty_like(big)
+tc = timeit(lambda: out.copy_(big))
+ta = timeit(lambda: torch.add(big, big2, out=out))
+nb = big.numel() * 2
+print(json.dumps({"copy_GBps": round(2 * nb / tc / 1e6), "add_GBps": round(3 * nb / ta / 1e6)}))
