@@ -304,3 +304,19 @@ def test_linear_gelu_fused_matches_reference():
     for got, ref in ((x.grad, xr.grad), (lin.weight.grad, wr.grad), (lin.bias.grad, br.grad)):
         rel = ((got.float() - ref).norm() / ref.norm()).item()
         assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("shape", [(7, 96), (4096, 1024), (8192, 3072), (3, 5, 4104)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bias_grad_single_launch(shape, dtype):
+    """Column sums with the last-block reduction (csrc/fused.hip): vs fp32 sums, repeated calls
+    (the ticket counters must reset themselves) and both output dtypes."""
+    import determined_amd.ops as ops
+
+    torch.manual_seed(0)
+    g = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+    ref = g.float().reshape(-1, shape[-1]).sum(0)
+    for _ in range(3):
+        out = ops.ext().bias_grad(g, dtype)
+        assert out.dtype == dtype and out.shape == (shape[-1],)
+        torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-1)
