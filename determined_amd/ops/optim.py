@@ -216,7 +216,8 @@ class _FusedBase(torch.optim.Optimizer):
         # sat idle).  Gradients are persistent bucket views, so a signature of the parameter /
         # gradient objects and their storage identifies a step whose plans are unchanged.
         # Stored in ``_plans``: every ``_plans.clear()`` (checkpoint load, re-shard) drops it.
-        sig = tuple((id(p), id(p.grad), p.grad.data_ptr()) if p.grad is not None else (id(p),)
+        # (parameter storage is part of it: ZeRO-3 style ``p.data`` swaps must rebuild the plan)
+        sig = tuple((p.data_ptr(), id(p.grad), p.grad.data_ptr()) if p.grad is not None else (p.data_ptr(),)
                     for g in self.param_groups for p in g["params"])
         fast = self._plans.get("__fast__")
         if fast is not None and fast[0] == sig:
