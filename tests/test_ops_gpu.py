@@ -320,3 +320,20 @@ def test_bias_grad_single_launch(shape, dtype):
         out = ops.ext().bias_grad(g, dtype)
         assert out.dtype == dtype and out.shape == (shape[-1],)
         torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-1)
+
+
+def test_fused_optimizer_plan_cache_tracks_storage():
+    """The cached step plan (fast host path) is rebuilt when a parameter's storage changes."""
+    import determined_amd.ops as ops
+
+    p = torch.nn.Parameter(torch.ones(1000, device="cuda"))
+    g = torch.ones_like(p)  # one persistent gradient object, as with bucket views
+    opt = ops.FusedSGD([p], lr=0.1, momentum=0.0, weight_decay=0.0)
+    for _ in range(2):
+        p.grad = g
+        opt.step()
+    torch.testing.assert_close(p.detach(), torch.full_like(p, 0.8))
+    p.data = torch.zeros(1000, device="cuda")  # new storage, same Parameter / gradient objects
+    p.grad = g
+    opt.step()
+    torch.testing.assert_close(p.detach(), torch.full_like(p, -0.1))
