@@ -67,10 +67,10 @@ void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, con
                         hipStream_t, const uint8_t*, const void*);
 void damd_bn_pool_fwd_launch(const void*, void*, uint8_t*, int64_t, int, int, int, int, int, const void*, const void*,
                              float*, float*, float, float, float*, float*, float*, float*, float*, int, int, hipStream_t,
-                             const float*, int);
+                             const float*, int, void*);
 void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, int, int, int, int, int, const float*,
                              const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
-                             hipStream_t, const void*);
+                             hipStream_t, const void*, const void*);
 void damd_hw_broadcast_launch(const void*, void*, int64_t, int64_t, int, float, int, hipStream_t);
 // launchers (conv_stem.hip)
 extern "C" int damd_stem_supported(int64_t, int64_t);
@@ -502,6 +502,8 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
   auto stats = at::empty({4, C}, fopts);
   auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto idx = at::empty({N * OH * OW * C}, x.options().dtype(at::kByte));
+  // input value at each window's argmax: lets the backward reduce run in the pooled domain
+  auto xarg = at::empty_like(y);
   // stats_part: (sum, sum sq) partials [nb, 2, C] already produced with x (stem_conv_fwd)
   const float* pre = nullptr;
   int pre_nb = 0;
@@ -517,13 +519,13 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
                           bias.data_ptr(), rm, rv, static_cast<float>(momentum), static_cast<float>(eps),
                           part.data_ptr<float>(), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
                           stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), dtype_code(x), dtype_code(weight),
-                          cur_stream(), pre, pre_nb);
-  return {y, idx, stats};
+                          cur_stream(), pre, pre_nb, xarg.data_ptr());
+  return {y, idx, stats, xarg};
 }
 
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& x,
                                     const at::Tensor& stats, const at::Tensor& weight,
-                                    const c10::optional<at::Tensor>& dp2) {
+                                    const c10::optional<at::Tensor>& dp2, const c10::optional<at::Tensor>& xarg) {
   TORCH_CHECK(x.dim() == 4 && bn_supported(x), "bn_pool_bwd: bad x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
@@ -545,11 +547,18 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx,
                 "bn_pool_bwd: dp2 must match dp");
     d2 = dp2->data_ptr();
   }
+  const void* xa = nullptr;
+  if (xarg.has_value() && xarg->defined()) {
+    TORCH_CHECK(xarg->sizes() == dp.sizes() && xarg->strides() == dp.strides() &&
+                xarg->scalar_type() == x.scalar_type() && xarg->device() == dp.device(),
+                "bn_pool_bwd: xarg must match dp");
+    xa = xarg->data_ptr();
+  }
   damd_bn_pool_bwd_launch(dp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), N, static_cast<int>(H),
                           static_cast<int>(W), static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW),
                           stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
                           stats[3].data_ptr<float>(), part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(),
-                          dbeta.data_ptr(), dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream(), d2);
+                          dbeta.data_ptr(), dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream(), d2, xa);
   return {dx, dgamma, dbeta};
 }
 

@@ -435,7 +435,8 @@ __device__ __forceinline__ int win_pos(int h, int w, int oh, int ow) { return (h
 template <typename T>
 __global__ void __launch_bounds__(kBNThreads)
 bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
-                           T* __restrict__ y, uint8_t* __restrict__ idx, int64_t Vout, int TPR, PoolGeo g) {
+                           T* __restrict__ y, uint8_t* __restrict__ idx, int64_t Vout, int TPR, PoolGeo g,
+                           T* __restrict__ xarg) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBNThreads;
   const int64_t T0 = static_cast<int64_t>(blockIdx.x) * kBNThreads + threadIdx.x;
   const int cg = static_cast<int>(T0 % TPR);  // stride is a multiple of TPR
@@ -448,10 +449,10 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
     const int ow = static_cast<int>(pix % g.OW);
     const int oh = static_cast<int>((pix / g.OW) % g.OH);
     const int64_t n = pix / (static_cast<int64_t>(g.OW) * g.OH);
-    float best[8];
+    float best[8], xa[8];
     int arg[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; xa[k] = 0.f; }
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int h = 2 * oh - 1 + kh;
@@ -465,7 +466,7 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float r = fmaxf(a[k] * sc[k] + sh[k], 0.f);
-          if (r > best[k]) { best[k] = r; arg[k] = kh * 3 + kw; }
+          if (r > best[k]) { best[k] = r; arg[k] = kh * 3 + kw; xa[k] = a[k]; }
         }
       }
     }
@@ -474,6 +475,64 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
 #pragma unroll
     for (int k = 0; k < 4; ++k) { lo |= static_cast<uint32_t>(arg[k]) << (8 * k); hi |= static_cast<uint32_t>(arg[k + 4]) << (8 * k); }
     *reinterpret_cast<uint2*>(idx + v * 8) = make_uint2(lo, hi);
+    if (xarg != nullptr) V8<T>::st(xarg + v * 8, xa);
+  }
+}
+
+// BN-backward reduce in the POOLED domain: every pooled gradient lands on exactly one input
+// pixel (its window's argmax) and dz is linear in it, so
+//   sum dz = sum_out dp [z_arg > 0],   sum dz (x - mean) = sum_out dp [z_arg > 0] (x_arg - mean)
+// with x_arg the input value at the argmax (written by the forward).  Reads dp + x_arg (a
+// quarter of the input each) instead of the full input plus the (dp, argmax) gathers.
+template <typename T>
+__global__ void __launch_bounds__(kBNThreads)
+pooled_bn_bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ dp2, const T* __restrict__ xarg,
+                            const float* __restrict__ mean, const float* __restrict__ scale,
+                            const float* __restrict__ shift, int64_t Q, int C, int64_t rows_per_block,
+                            float* __restrict__ part) {
+  const Geo geo_ = geo(C);
+  const int tid = threadIdx.x;
+  const int cg0 = geo_.TPR <= kBNThreads ? tid % geo_.TPR : tid;
+  const int rsub = geo_.TPR <= kBNThreads ? tid / geo_.TPR : 0;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(Q, r0 + rows_per_block);
+  __shared__ float red[kBNThreads * 8];
+  for (int gi = 0; gi < geo_.G; ++gi) {
+    const int cg = cg0 + gi * kBNThreads;
+    float mu[8], sc[8], sh[8], s[8], sx[8];
+    V8<float>::ld(mean + cg * 8, mu);
+    V8<float>::ld(scale + cg * 8, sc);
+    V8<float>::ld(shift + cg * 8, sh);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; sx[k] = 0.f; }
+    for (int64_t q = r0 + rsub; q < r1; q += geo_.RS) {
+      const int64_t off = q * C + cg * 8;
+      float d[8], a[8];
+      V8<T>::ld(dp + off, d);
+      if (dp2 != nullptr) add_v8(dp2 + off, d);
+      V8<T>::ld(xarg + off, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? d[k] : 0.f;
+        s[k] += dz;
+        sx[k] += dz * (a[k] - mu[k]);
+      }
+    }
+    for (int which = 0; which < 2; ++which) {
+      float* v = which == 0 ? s : sx;
+      if (geo_.RS > 1) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[tid * 8 + k] = v[k];
+        __syncthreads();
+        if (rsub == 0) {
+          for (int qq = 1; qq < geo_.RS; ++qq)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += red[(qq * geo_.TPR + cg0) * 8 + k];
+        }
+      }
+      if (rsub == 0) V8<float>::st(part + (static_cast<int64_t>(blockIdx.x) * 2 + which) * C + cg * 8, v);
+    }
   }
 }
 
@@ -818,7 +877,7 @@ void damd_hw_broadcast_launch(const void* g, void* out, int64_t N, int64_t HW, i
 void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, int H, int W, int C, int OH, int OW,
                              const void* w, const void* b, float* run_mean, float* run_var, float momentum, float eps,
                              float* part, float* mean, float* invstd, float* scale, float* shift, int x_dtype,
-                             int w_dtype, hipStream_t st, const float* pre_part, int pre_nb) {
+                             int w_dtype, hipStream_t st, const float* pre_part, int pre_nb, void* xarg) {
   const int64_t M = N * H * W;
   int nb;
   int64_t rpb = rows_per_block_for(M, C, &nb);
@@ -845,23 +904,30 @@ void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, in
   const dim3 ag(apply_grid(Vout, TPR));
   if (x_dtype == 1)
     hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift,
-                       static_cast<bf16_t*>(y), idx, Vout, TPR, g);
+                       static_cast<bf16_t*>(y), idx, Vout, TPR, g, static_cast<bf16_t*>(xarg));
   else
     hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift,
-                       static_cast<float*>(y), idx, Vout, TPR, g);
+                       static_cast<float*>(y), idx, Vout, TPR, g, static_cast<float*>(xarg));
   DAMD_CHECK_LAUNCH();
 }
 
 void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, int64_t N, int H, int W, int C, int OH,
                              int OW, const float* mean, const float* invstd, const float* scale, const float* shift,
                              float* part, float* coef, void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype,
-                             hipStream_t st, const void* dp2) {
+                             hipStream_t st, const void* dp2, const void* xarg) {
   const int64_t M = N * H * W;      // BN statistics count
   const int64_t Q = N * OH * OW;    // quads (rows of the fused backward kernels)
   int nb;
   const int64_t rpb = rows_per_block_for(Q, C, &nb);
   const PoolGeo g{H, W, OH, OW};
-  if (x_dtype == 1)
+  if (xarg != nullptr) {  // pooled-domain reduce (argmax input values saved by the forward)
+    if (x_dtype == 1)
+      hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp),
+                         static_cast<const bf16_t*>(dp2), static_cast<const bf16_t*>(xarg), mean, scale, shift, Q, C, rpb, part);
+    else
+      hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp),
+                         static_cast<const float*>(dp2), static_cast<const float*>(xarg), mean, scale, shift, Q, C, rpb, part);
+  } else if (x_dtype == 1)
     hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
                        static_cast<const bf16_t*>(x), mean, scale, shift, Q, C, rpb, part, g);
   else

@@ -73,10 +73,10 @@ class _BNReLUPoolFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, split=False, stats_part=None):
         from determined_amd import ops
 
-        y, idx, stats = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum), float(eps),
-                                              stats_part)
-        ctx.save_for_backward(x, idx, stats, weight)
-        ctx.mark_non_differentiable(idx)
+        y, idx, stats, xarg = ops.ext().bn_pool_fwd(x, weight, bias, running_mean, running_var, float(momentum),
+                                                    float(eps), stats_part)
+        ctx.save_for_backward(x, idx, stats, weight, xarg)
+        ctx.mark_non_differentiable(idx, xarg)
         if split:
             return y, y.detach()
         return y
@@ -85,11 +85,11 @@ class _BNReLUPoolFn(torch.autograd.Function):
     def backward(ctx, dy, dy2=None):
         from determined_amd import ops
 
-        x, idx, stats, weight = ctx.saved_tensors
+        x, idx, stats, weight, xarg = ctx.saved_tensors
         dy, dy2 = _sum_grads(dy, dy2, torch.channels_last)
         if dy is None:
             return (None,) * 9
-        dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight, dy2)
+        dx, dg, db = ops.ext().bn_pool_bwd(dy, idx, x, stats, weight, dy2, xarg)
         return dx, dg, db, None, None, None, None, None, None
 
 
