@@ -14,7 +14,7 @@ from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 from determined_amd.ops import fusion_enabled
-from determined_amd.ops.conv import stem_conv2d
+from determined_amd.ops.conv import conv1x1 as conv1x1_fwd, stem_conv2d
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -44,9 +44,9 @@ class Bottleneck(nn.Module):
         ``split_grad`` makes this block's output such a pair (ops/bn.py)."""
         xm, xs = x if isinstance(x, tuple) else (x, x)
         identity = xs if self.downsample is None else self.downsample(xs)
-        out = self.bn1(self.conv1(xm))
+        out = self.bn1(conv1x1_fwd(self.conv1, xm))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity, split_grad=split_grad)
+        return self.bn3(conv1x1_fwd(self.conv3, out), identity, split_grad=split_grad)
 
 
 class BasicBlock(nn.Module):

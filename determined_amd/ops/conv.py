@@ -61,3 +61,54 @@ def stem_conv2d(conv: nn.Conv2d, x: torch.Tensor, with_stats: bool = False):
         return y, (part if stats else None)
     y = conv(x)
     return (y, None) if with_stats else y
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    """1x1 stride-1 convolution whose input gradient is one GEMM.  A channels-last activation is
+    an [N*H*W, C] row-major matrix, so dX = dY @ W on hipBLASLt writes dX directly, where
+    MIOpen's solvers zero-fill dX and then run a CK/igemm kernel.  The forward and the weight
+    gradient stay on MIOpen (dW as dY^T @ X has K = N*H*W and is 2-15x slower as a GEMM).
+    Measured per shape at batch 512: profiles/conv1x1_gemm_ab_b512_1gpu.jsonl."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x, weight)
+        return torch.nn.functional.conv2d(x, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        n, cout, h, w = dy.shape
+        cin = x.shape[1]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            dx = (dy2 @ weight.view(cout, cin)).view(n, h, w, cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        return dx, dw
+
+
+def conv1x1_gemm_wins(hw: int, cin: int, cout: int) -> bool:
+    """Shapes where the GEMM input gradient beat MIOpen on MI355X at batch 512
+    (profiles/conv1x1_gemm_ab_b512_1gpu.jsonl): every 14x14 / 7x7 layer, and the channel-reducing
+    layers at 56x56 / 28x28."""
+    return hw <= 14 or cin > cout
+
+
+def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """``conv(x)`` for a bias-free 1x1 stride-1 convolution; bf16 channels-last inputs on the GPU
+    take :class:`_Conv1x1Fn` where its GEMM input gradient is faster (``DAMD_DISABLE_FUSIONS=
+    conv1x1_gemm`` turns it off)."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16 and x.dim() == 4
+            and conv.bias is None and conv.groups == 1 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.dilation == (1, 1) and x.requires_grad
+            and x.is_contiguous(memory_format=torch.channels_last) and torch.is_grad_enabled()
+            and conv1x1_gemm_wins(x.shape[2], conv.in_channels, conv.out_channels)):
+        from determined_amd import ops
+
+        if ops.fusion_enabled("conv1x1_gemm"):
+            return _Conv1x1Fn.apply(x, conv.weight)
+    return conv(x)

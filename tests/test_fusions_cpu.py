@@ -71,3 +71,13 @@ def test_disable_fusions_env_switch():
     env = dict(os.environ, PYTHONPATH=ROOT, DAMD_DISABLE_FUSIONS="split_grad, stem_conv")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     assert out.stdout.split() == ["False", "False", "True"]
+
+
+def test_conv1x1_gemm_path_falls_back_on_cpu():
+    from determined_amd.ops.conv import conv1x1, conv1x1_gemm_wins
+
+    conv = torch.nn.Conv2d(32, 16, 1, bias=False)
+    x = torch.randn(2, 32, 7, 7, requires_grad=True)
+    torch.testing.assert_close(conv1x1(conv, x), conv(x))
+    assert conv1x1_gemm_wins(14, 64, 256) and conv1x1_gemm_wins(56, 256, 64)
+    assert not conv1x1_gemm_wins(56, 64, 256) and not conv1x1_gemm_wins(28, 128, 512)

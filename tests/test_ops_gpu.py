@@ -337,3 +337,24 @@ def test_fused_optimizer_plan_cache_tracks_storage():
     p.grad = g
     opt.step()
     torch.testing.assert_close(p.detach(), torch.full_like(p, -0.1))
+
+
+@pytest.mark.parametrize("hw,cin,cout", [(14, 64, 128), (28, 128, 32), (7, 96, 48)])
+def test_conv1x1_gemm_backward_matches_fp32(ops, hw, cin, cout):
+    from determined_amd.ops.conv import conv1x1
+
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(cin, cout, 1, bias=False).cuda().to(torch.bfloat16)
+    x = torch.randn(6, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    dy = torch.randn(6, cout, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = conv1x1(conv, x)
+    assert y.grad_fn is not None and "_Conv1x1Fn" in type(y.grad_fn).__name__
+    y.backward(dy.to(torch.bfloat16))
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().float().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, wr).backward(dy.to(torch.bfloat16).float())
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
+    torch.testing.assert_close(conv.weight.grad.float(), wr.grad, rtol=2e-2,
+                               atol=2e-2 * wr.grad.abs().max().item())
