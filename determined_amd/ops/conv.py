@@ -67,8 +67,10 @@ class _Conv1x1Fn(torch.autograd.Function):
     """1x1 stride-1 convolution whose input gradient is one GEMM.  A channels-last activation is
     an [N*H*W, C] row-major matrix, so dX = dY @ W on hipBLASLt writes dX directly, where
     MIOpen's solvers zero-fill dX and then run a CK/igemm kernel.  The forward and the weight
-    gradient stay on MIOpen (dW as dY^T @ X has K = N*H*W and is 2-15x slower as a GEMM).
-    Measured per shape at batch 512: profiles/conv1x1_gemm_ab_b512_1gpu.jsonl."""
+    gradient stay on MIOpen (dW as dY^T @ X has K = N*H*W and is 2-15x slower as a GEMM; the
+    forward as X @ W^T wins only on the channel-reducing 14x14/7x7 layers, ~0.15 ms/step total).
+    Measured per shape at batch 512: profiles/conv1x1_gemm_ab_b512_1gpu.jsonl,
+    profiles/conv1x1_fwd_gemm_ab_b512_1gpu.jsonl."""
 
     @staticmethod
     def forward(ctx, x, weight):
