@@ -31,7 +31,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("DAMD_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip"]
+HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip", "conv_igemm.hip"]
 # MFMA kernels whose accumulators are also touched by VALU code (online softmax, rescales):
 # keep them in the unified VGPR file instead of AGPRs, which otherwise costs a
 # v_accvgpr_read/write pair per element per tile (attention: 450 copies per kv tile) and

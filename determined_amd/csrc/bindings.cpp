@@ -56,10 +56,17 @@ int damd_resid_norm_bwd_launch(const void*, const void*, const void*, const floa
                                const uint8_t*, float, void*, void*, float*, float*, int64_t, int, int, int,
                                hipStream_t);
 void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
+// launchers (conv_igemm.hip)
+extern "C" int damd_conv_num_cfgs();
+extern "C" int damd_conv_default_cfg(int, int64_t);
+extern "C" int damd_conv_supported(int, int, int);
+extern "C" int damd_conv_groups(int64_t, int, int, int);
+extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
+                                    int, int, int, hipStream_t);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
-                        float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*);
+                        float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*, const float*, int);
 void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
                                hipStream_t);
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
@@ -322,7 +329,8 @@ bool bn_supported(const at::Tensor& x) {
 std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                                    const c10::optional<at::Tensor>& running_mean,
                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps,
-                                   const c10::optional<at::Tensor>& residual, bool relu, bool want_mask) {
+                                   const c10::optional<at::Tensor>& residual, bool relu, bool want_mask,
+                                   const c10::optional<at::Tensor>& stats_part) {
   TORCH_CHECK(bn_supported(x), "bn_act_fwd: unsupported input layout/shape");
   const int64_t C = bn_channels(x);
   const int64_t M = x.numel() / C;
@@ -342,7 +350,17 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
     rv = running_var->data_ptr<float>();
   }
   auto fopts = x.options().dtype(at::kFloat);
-  const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
+  // stats_part: (sum, sum sq) partials [nb, 2, C] the producer of x already computed (conv_fwd)
+  const float* pre = nullptr;
+  int pre_nb = 0;
+  if (stats_part.has_value() && stats_part->defined()) {
+    TORCH_CHECK(stats_part->scalar_type() == at::kFloat && stats_part->dim() == 3 && stats_part->size(1) == 2 &&
+                stats_part->size(2) == C && stats_part->is_contiguous() && stats_part->device() == x.device(),
+                "bn_act_fwd: stats_part must be a float32 [nb, 2, C] tensor");
+    pre = stats_part->data_ptr<float>();
+    pre_nb = static_cast<int>(stats_part->size(0));
+  }
+  const int nb = pre ? 1 : damd_bn_num_blocks(M, static_cast<int>(C));
   auto part = at::empty({nb, 2, C}, fopts);
   auto stats = at::empty({4, C}, fopts);  // mean, invstd, scale, shift
   auto y = at::empty_like(x);
@@ -354,7 +372,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
                      static_cast<float>(momentum), static_cast<float>(eps), part.data_ptr<float>(),
                      stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
                      stats[3].data_ptr<float>(), relu, dtype_code(x), dtype_code(weight), cur_stream(),
-                     mk ? mask.data_ptr<uint8_t>() : nullptr);
+                     mk ? mask.data_ptr<uint8_t>() : nullptr, pre, pre_nb);
   return {y, stats, mask};
 }
 
@@ -616,6 +634,39 @@ at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::
   return w.is_contiguous(at::MemoryFormat::ChannelsLast) ? dw : dw.contiguous();
 }
 
+// ---------------------------------------------------------------- implicit-GEMM convolution
+// x: [N, C, H, W] bf16 channels-last; w: [K, C, R, S] bf16 (made channels-last = [K][R][S][C]);
+// returns (y [N, K, OH, OW] channels-last, stats partials [groups, 2, K] or an empty tensor).
+bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
+  if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
+  return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+         w.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.size(1) == x.size(1) &&
+         damd_conv_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(cfg));
+}
+
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 bool want_stats, int64_t cfg, int64_t groups) {
+  if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
+  TORCH_CHECK(conv_supported(x, w, cfg), "conv_fwd: unsupported input / weight / config");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t K = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(stride >= 1 && pad >= 0 && H + 2 * pad >= R && W + 2 * pad >= S, "conv_fwd: bad geometry");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = N * OH * OW;
+  TORCH_CHECK(M < (int64_t{1} << 31) - 4096 && x.numel() < (int64_t{1} << 40), "conv_fwd: tensor too large");
+  auto wl = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(cfg), static_cast<int>(groups));
+  at::Tensor part = want_stats ? at::empty({G, 2, K}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
+  const int rc = damd_conv_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
+                                      static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                      static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
+                                      static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream());
+  TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
+  return {y, part};
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -788,6 +839,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resid_norm_bwd", &resid_norm_bwd);
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("global_avgpool_bwd", &global_avgpool_bwd);
+  m.def("conv_supported", &conv_supported);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_num_cfgs", &damd_conv_num_cfgs);
+  m.def("conv_default_cfg", [](int64_t K) { return damd_conv_default_cfg(static_cast<int>(K), 0); });
   m.def("stem_conv_supported", &stem_conv_supported);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);

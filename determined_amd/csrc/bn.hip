@@ -727,19 +727,25 @@ int damd_bn_num_blocks(int64_t M, int C) {
 void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int C, const void* w, const void* b,
                         float* run_mean, float* run_var, float momentum, float eps, float* part, float* mean,
                         float* invstd, float* scale, float* shift, int relu, int x_dtype, int w_dtype,
-                        hipStream_t st, uint8_t* mask) {
+                        hipStream_t st, uint8_t* mask, const float* pre_part, int pre_nb) {
   int nb;
   const int64_t rpb = rows_per_block_for(M, C, &nb);
-  if (x_dtype == 1)
+  const void* pilot = x;
+  if (pre_part != nullptr) {  // plain (sum, sum sq) partials from the producing convolution
+    part = const_cast<float*>(pre_part);
+    nb = pre_nb;
+    pilot = nullptr;
+  } else if (x_dtype == 1) {
     hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
-  else
+  } else {
     hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+  }
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, x, x_dtype == 1, momentum, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
   const int TPR = C / 8;
   const int64_t V = M * C / 8;

@@ -1,0 +1,367 @@
+// Implicit-GEMM convolution for gfx950 / MI355X: bf16 NHWC activations, [K][R][S][C] weights
+// (PyTorch's channels-last weight layout), fp32 accumulation on MFMA.
+//
+// One kernel serves the forward convolution and the stride-1 input gradient (the latter is the
+// forward convolution of dY with the flipped, transposed weights), with an optional epilogue
+// that emits the per-output-channel (sum, sum of squares) partials the following BatchNorm
+// needs -- which removes BatchNorm's separate statistics pass over the conv output.
+//
+// GEMM view (C^T formulation): out^T[co][pixel] = W[co][k] . im2col^T[k][pixel], k = (r, s, c).
+// Both operands are k-contiguous rows in memory (weight rows; one input pixel's 64 channels for
+// one tap), so both are staged into LDS by the direct global->LDS DMA
+// (`global_load_lds_dwordx4`, 16 B per lane, 8 rows of 128 B per wave-instruction) with a per-lane
+// source address that does the im2col gather and points padding / tail rows at a zero page.
+// MFMA v_mfma_f32_16x16x32_bf16: A = weight rows (co), B = pixel rows; lane l holds
+// C[co = 4(l>>4) + r][pixel = l&15], so after permuting which weight row feeds which A row a lane
+// ends with 8 consecutive output channels of one pixel and writes them as one 16-byte store.
+//
+// LDS image: [rows][64] bf16, 128-byte rows, 16-byte chunk c of row r stored at slot
+// c ^ f(r), f(r) = ((r >> 1) ^ (r >> 3)) & 7 -- conflict-free for the ds_read_b128 lane groups of
+// both the permuted weight rows and the consecutive pixel rows (checked against the gfx950
+// lane-group table).  The DMA writes LDS linearly, so the swizzle is applied to the per-lane
+// SOURCE address (chunk = slot ^ f(row)) and again on the read.
+//
+// Schedule: persistent blocks.  Block -> (co tile, pixel group) with the co tiles of one pixel
+// group on one XCD (they read the same input rows through that XCD's L2); each block walks the
+// pixel tiles grp, grp + groups, ...  The (tile, k-step) stream is flattened and double-buffered:
+// the DMA for item i+1 is in flight while item i computes, including across tile boundaries, so
+// K = 64 layers (one k-step per tile) still overlap their loads with the previous tile's MFMAs
+// and stores.
+
+#include "common.h"
+
+namespace damd {
+namespace igemm {
+
+typedef short s8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kBK = 64;        // k elements per stage: 64 channels of one tap
+
+// 128 zero bytes: the DMA source of padding / out-of-range rows (read-only).
+__device__ __attribute__((aligned(128))) uint4 g_zero_rows[8];
+
+struct Geo {
+  int H, W, C;       // input (C % 64 == 0)
+  int OH, OW, K;     // output (K % BCO == 0)
+  int R, S, stride, pad;
+  int64_t M;         // N * OH * OW
+  int cblk;          // C / 64
+  int ksteps;        // R * S * cblk
+  int ptiles, ctiles, groups;
+};
+
+__device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
+
+__device__ __forceinline__ void dma16(const void* src, bf16_t* lds_base) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+// A-operand row (output channel within the wave's co range) of fragment i for fragment row rho:
+// fragment pair (2q, 2q+1) covers 32 channels and lane group g ends with channels 8g..8g+7.
+__device__ __forceinline__ int a_row(int i, int rho) {
+  return 32 * (i >> 1) + 8 * (rho >> 2) + 4 * (i & 1) + (rho & 3);
+}
+
+template <int BCO, int BP, int WCO, bool STATS>
+__global__ void __launch_bounds__(kThreads, 2)
+conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                float* __restrict__ part, Geo g) {
+  constexpr int WP = 4 / WCO;
+  constexpr int TCO = BCO / WCO, TP = BP / WP;
+  constexpr int FI = TCO / 16, FJ = TP / 16;
+  static_assert(WCO * WP == 4 && FI % 2 == 0 && FJ >= 1 && BCO % 32 == 0 && BP % 32 == 0, "bad tile");
+  constexpr int STAGE = (BCO + BP) * kBK;  // elements per stage
+  constexpr int NIW = BCO / 32, NIX = BP / 32;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rho = lane & 15, lg = lane >> 4;
+  const int wco0 = (wave % WCO) * TCO, wp0 = (wave / WCO) * TP;
+
+  // block -> (co tile, pixel group); consecutive remapped ids share an XCD (bijective remap)
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ct = rid % g.ctiles, grp = rid / g.ctiles;
+  const int ntiles = grp < g.ptiles ? (g.ptiles - grp + g.groups - 1) / g.groups : 0;
+  const int items = ntiles * g.ksteps;
+  const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
+
+  // ---- DMA lane roles: lane -> (row within its 8-row piece, 16-byte slot)
+  const int prow = lane >> 3, slot = lane & 7;
+  const bf16_t* wsrc[NIW];
+#pragma unroll
+  for (int i = 0; i < NIW; ++i) {
+    const int co = 8 * (wave + 4 * i) + prow;
+    wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
+  }
+  // pixel rows: per tile (image offset + chunk, top-left input coordinate, validity)
+  int64_t xoff[NIX];
+  int ih0[NIX], iw0[NIX];
+  const int OHW = g.OH * g.OW;
+  auto tile_rows = [&](int pt) {
+#pragma unroll
+    for (int i = 0; i < NIX; ++i) {
+      const int p = 8 * (wave + 4 * i) + prow;
+      const int m = pt * BP + p;  // M < 2^31 (host-checked)
+      if (m < g.M) {
+        const int n = m / OHW;
+        const int rem = m - n * OHW;
+        const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
+        ih0[i] = oh * g.stride - g.pad;
+        iw0[i] = ow * g.stride - g.pad;
+        xoff[i] = static_cast<int64_t>(n) * g.H * g.W * g.C + ((slot ^ swz(p)) << 3);
+      } else {
+        ih0[i] = -0x40000000;  // never in range
+        iw0[i] = 0;
+        xoff[i] = 0;
+      }
+    }
+  };
+
+  // load-side counters: tile, channel block, tap (r, s)
+  int l_tile = 0, l_cb = 0, l_r = 0, l_s = 0, l_ks = 0;
+  auto issue = [&](int stage) {
+    bf16_t* sw = lds + stage * STAGE;
+    const int pt = grp + l_tile * g.groups;
+    if (l_ks == 0) tile_rows(pt);
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + 4 * i) * kBK);
+    const int c0 = l_cb * kBK;
+#pragma unroll
+    for (int i = 0; i < NIX; ++i) {
+      const int ih = ih0[i] + l_r, iw = iw0[i] + l_s;
+      const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
+      const bf16_t* src = ok ? x + xoff[i] + (static_cast<int64_t>(ih) * g.W + iw) * g.C + c0
+                             : reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+      dma16(src, sw + (BCO + 8 * (wave + 4 * i)) * kBK);
+    }
+    // advance (cb fastest, then s, then r, then tile)
+    if (++l_cb == g.cblk) {
+      l_cb = 0;
+      if (++l_s == g.S) {
+        l_s = 0;
+        if (++l_r == g.R) l_r = 0;
+      }
+    }
+    if (++l_ks == g.ksteps) { l_ks = 0; ++l_tile; }
+  };
+
+  f4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float st_s[FI / 2][8], st_q[FI / 2][8];
+  if (STATS) {
+#pragma unroll
+    for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
+  }
+
+  if (items > 0) issue(0);
+  int c_ks = 0, c_tile = 0;
+  for (int it = 0; it < items; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage it&1 landed for every wave; stage (it+1)&1 is no longer read
+    if (it + 1 < items) issue((it + 1) & 1);
+    const bf16_t* sw = lds + (it & 1) * STAGE;
+    const bf16_t* sx = sw + BCO * kBK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lg;
+      s8 a[FI], b[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int row = wco0 + a_row(i, rho);
+        a[i] = *reinterpret_cast<const s8*>(sw + row * kBK + ((chunk ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int row = wp0 + 16 * j + rho;
+        b[j] = *reinterpret_cast<const s8*>(sx + row * kBK + ((chunk ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+    if (++c_ks == g.ksteps) {
+      // epilogue: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel wp0 + 16j + rho
+      const int64_t pt = grp + static_cast<int64_t>(c_tile) * g.groups;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int64_t m = pt * BP + wp0 + 16 * j + rho;
+        const bool ok = m < g.M;
+#pragma unroll
+        for (int q = 0; q < FI / 2; ++q) {
+          bf16x8 v;
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const u16v2_t p0 = f2bf2(acc[2 * q][j][e], acc[2 * q][j][e + 1]);
+            const u16v2_t p1 = f2bf2(acc[2 * q + 1][j][e], acc[2 * q + 1][j][e + 1]);
+            v.v[e] = p0[0]; v.v[e + 1] = p0[1];
+            v.v[4 + e] = p1[0]; v.v[5 + e] = p1[1];
+          }
+          if (ok) {
+            *reinterpret_cast<bf16x8*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg) = v;
+            if (STATS) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float f = bf2f(v.v[e]);
+                st_s[q][e] += f;
+                st_q[q][e] += f * f;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      c_ks = 0;
+      ++c_tile;
+    }
+  }
+
+  if (STATS) {
+    // sum over the 16 pixel lanes of each lane group, then over the WP waves sharing a co range
+#pragma unroll
+    for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          st_s[q][e] += __shfl_xor(st_s[q][e], o, 64);
+          st_q[q][e] += __shfl_xor(st_q[q][e], o, 64);
+        }
+    __syncthreads();  // LDS reuse: every wave is past its last fragment read
+    float* red = reinterpret_cast<float*>(lds);  // [WP][2][BCO]
+    const int wpi = wave / WCO;
+    if (rho == 0) {
+#pragma unroll
+      for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int co = wco0 + 32 * q + 8 * lg + e;
+          red[(wpi * 2) * BCO + co] = st_s[q][e];
+          red[(wpi * 2 + 1) * BCO + co] = st_q[q][e];
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 2 * BCO; t += kThreads) {
+      const int which = t / BCO, co = t - which * BCO;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < WP; ++k) s += red[(k * 2 + which) * BCO + co];
+      part[(static_cast<int64_t>(grp) * 2 + which) * g.K + static_cast<int64_t>(ct) * BCO + co] = s;
+    }
+  }
+}
+
+// Per-config resources: LDS bytes per block (for the residency estimate).
+template <int BCO, int BP>
+constexpr int lds_bytes() { return 2 * (BCO + BP) * kBK * 2; }
+
+}  // namespace igemm
+}  // namespace damd
+
+using namespace damd;
+using namespace damd::igemm;
+
+namespace {
+
+struct Cfg {
+  int bco, bp, wco;
+};
+// cfg ids: 0: 64x128 (1x4 waves), 1: 128x128 (2x2), 2: 128x256 (2x2), 3: 64x256 (1x4), 4: 256x128 (4x1)
+constexpr Cfg kCfgs[] = {{64, 128, 1}, {128, 128, 2}, {128, 256, 2}, {64, 256, 1}, {256, 128, 4}};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+int blocks_per_cu(int bco, int bp) {
+  const int lds = 2 * (bco + bp) * kBK * 2;
+  int occ = (160 * 1024) / lds;
+  if (occ > 2) occ = 2;  // __launch_bounds__(256, 2)
+  return occ < 1 ? 1 : occ;
+}
+
+}  // namespace
+
+extern "C" {
+
+int damd_conv_num_cfgs() { return kNumCfgs; }
+
+// Heuristic default config for a layer: widest co tile the channel count allows.
+int damd_conv_default_cfg(int K, int64_t M) {
+  (void)M;
+  if (K % 128 == 0) return 1;
+  return 0;
+}
+
+int damd_conv_supported(int C, int K, int cfg) {
+  if (cfg < 0 || cfg >= kNumCfgs) return 0;
+  return C % kBK == 0 && C > 0 && K % kCfgs[cfg].bco == 0;
+}
+
+// groups (pixel-tile strides) for a config; also the leading dim of the stats partials
+int damd_conv_groups(int64_t M, int K, int cfg, int groups_override) {
+  const Cfg c = kCfgs[cfg];
+  const int64_t ptiles = (M + c.bp - 1) / c.bp;
+  const int ctiles = K / c.bco;
+  int64_t groups = groups_override > 0 ? groups_override
+                                       : (256LL * blocks_per_cu(c.bco, c.bp) + ctiles - 1) / ctiles;
+  if (groups > ptiles) groups = ptiles;
+  if (groups < 1) groups = 1;
+  return static_cast<int>(groups);
+}
+
+// x: [N, H, W, C] bf16; w: [K, R, S, C] bf16; y: [N, OH, OW, K] bf16;
+// part: null or [groups][2][K] fp32 (sum, sum of squares of the bf16 outputs)
+int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                         int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st) {
+  if (!damd_conv_supported(C, K, cfg)) return -1;
+  const Cfg c = kCfgs[cfg];
+  Geo g;
+  g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
+  g.OH = (H + 2 * pad - R) / stride + 1;
+  g.OW = (W + 2 * pad - S) / stride + 1;
+  g.M = static_cast<int64_t>(N) * g.OH * g.OW;
+  g.cblk = C / kBK;
+  g.ksteps = R * S * g.cblk;
+  g.ptiles = static_cast<int>((g.M + c.bp - 1) / c.bp);
+  g.ctiles = K / c.bco;
+  g.groups = groups;
+  const dim3 grid(static_cast<unsigned>(g.ctiles * groups));
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* wp = static_cast<const bf16_t*>(w);
+  bf16_t* yp = static_cast<bf16_t*>(y);
+#define L(BCO, BP, WCO)                                                                                       \
+  do {                                                                                                        \
+    if (part) hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, true>), grid, dim3(kThreads), 0, st, xp, wp, yp, part, g); \
+    else hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, false>), grid, dim3(kThreads), 0, st, xp, wp, yp, part, g);     \
+  } while (0)
+  switch (cfg) {
+    case 0: L(64, 128, 1); break;
+    case 1: L(128, 128, 2); break;
+    case 2: L(128, 256, 2); break;
+    case 3: L(64, 256, 1); break;
+    default: L(256, 128, 4); break;
+  }
+#undef L
+  DAMD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

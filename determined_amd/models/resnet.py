@@ -14,7 +14,7 @@ from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 from determined_amd.ops import fusion_enabled
-from determined_amd.ops.conv import conv1x1 as conv1x1_fwd, stem_conv2d
+from determined_amd.ops.conv import conv_bn_input, stem_conv2d
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -23,6 +23,17 @@ def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _downsample(ds: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """``ds(x)`` for the ``Sequential(conv1x1, BatchNormAct2d)`` shortcut, with the BN statistics
+    from the conv epilogue."""
+    if (isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[1], BatchNormAct2d)
+            and not ds._forward_hooks and not ds._forward_pre_hooks and not ds[1]._forward_hooks
+            and not ds[1]._forward_pre_hooks):
+        y, part = conv_bn_input(ds[0], x)
+        return ds[1](y, stats_part=part)
+    return ds(x)
 
 
 class Bottleneck(nn.Module):
@@ -41,12 +52,16 @@ class Bottleneck(nn.Module):
 
     def forward(self, x, split_grad: bool = False):
         """``x`` is a tensor or the ``(main, shortcut)`` pair of a split-gradient producer;
-        ``split_grad`` makes this block's output such a pair (ops/bn.py)."""
+        ``split_grad`` makes this block's output such a pair (ops/bn.py).  Every conv hands its
+        output's BatchNorm statistics to the BN from its epilogue (ops/conv.py conv_bn_input)."""
         xm, xs = x if isinstance(x, tuple) else (x, x)
-        identity = xs if self.downsample is None else self.downsample(xs)
-        out = self.bn1(conv1x1_fwd(self.conv1, xm))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(conv1x1_fwd(self.conv3, out), identity, split_grad=split_grad)
+        identity = xs if self.downsample is None else _downsample(self.downsample, xs)
+        y, part = conv_bn_input(self.conv1, xm)
+        out = self.bn1(y, stats_part=part)
+        y, part = conv_bn_input(self.conv2, out)
+        out = self.bn2(y, stats_part=part)
+        y, part = conv_bn_input(self.conv3, out)
+        return self.bn3(y, identity, split_grad=split_grad, stats_part=part)
 
 
 class BasicBlock(nn.Module):
@@ -62,9 +77,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x, split_grad: bool = False):
         xm, xs = x if isinstance(x, tuple) else (x, x)
-        identity = xs if self.downsample is None else self.downsample(xs)
-        out = self.bn1(self.conv1(xm))
-        return self.bn2(self.conv2(out), identity, split_grad=split_grad)
+        identity = xs if self.downsample is None else _downsample(self.downsample, xs)
+        y, part = conv_bn_input(self.conv1, xm)
+        out = self.bn1(y, stats_part=part)
+        y, part = conv_bn_input(self.conv2, out)
+        return self.bn2(y, identity, split_grad=split_grad, stats_part=part)
 
 
 class ResNet(nn.Module):

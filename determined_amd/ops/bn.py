@@ -32,13 +32,15 @@ def _sum_grads(a, b, mf):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, split=False):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, split=False,
+                stats_part=None):
         from determined_amd import ops
 
         # residual + ReLU: the forward also emits a 1-bit-per-element ReLU mask, so the backward
-        # reads M*C/8 bytes instead of the residual tensor in both of its passes
+        # reads M*C/8 bytes instead of the residual tensor in both of its passes.
+        # stats_part: batch-statistic partials from the producing convolution (ops/conv.py)
         y, stats, mask = ops.ext().bn_act_fwd(x, weight, bias, running_mean, running_var, float(momentum),
-                                              float(eps), residual, bool(relu), True)
+                                              float(eps), residual, bool(relu), True, stats_part)
         masked = mask.numel() > 0
         ctx.save_for_backward(x, None if masked else residual, stats, weight, mask if masked else None)
         ctx.relu = relu
@@ -55,13 +57,13 @@ class _BNActFn(torch.autograd.Function):
         mf = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy, dy2 = _sum_grads(dy, dy2, mf)
         if dy is None:
-            return (None,) * 10
+            return (None,) * 11
         if dy2 is not None and mask is None:  # unmasked path: plain sum
             dy, dy2 = dy + dy2, None
         dx, dg, db, dres = ops.ext().bn_act_bwd(dy, x, residual, stats, weight, bool(ctx.relu), bool(ctx.has_res),
                                                 mask, dy2)
         return (dx, dg, db, None, None,
-                dres if ctx.has_res else None, None, None, None, None)
+                dres if ctx.has_res else None, None, None, None, None, None)
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -161,13 +163,17 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
         self._nbt_host = None
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, split_grad: bool = False):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, split_grad: bool = False,
+                stats_part: Optional[torch.Tensor] = None):
         """``relu(bn(x) [+ residual])``; with ``split_grad`` a pair ``(y, y)`` of handles whose
-        gradients are summed inside the fused backward (module docstring)."""
-        y = self._forward(x, residual, split_grad)
+        gradients are summed inside the fused backward (module docstring).  ``stats_part``: the
+        [nb, 2, C] (sum, sum of squares) partials of ``x`` its producer already computed
+        (``ops.conv.conv_bn_input``); training mode then skips the statistics pass."""
+        y = self._forward(x, residual, split_grad, stats_part)
         return y if not split_grad or isinstance(y, tuple) else (y, y)
 
-    def _forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], split: bool):
+    def _forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], split: bool,
+                 stats_part: Optional[torch.Tensor] = None):
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
             self._nbt_host = self._nbt() + 1
@@ -185,7 +191,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
             rv = self.running_var if self.track_running_stats else None
             # the in-kernel gradient sum needs the masked (residual + ReLU) backward
             split = split and residual is not None and self.act
-            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act, split)
+            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act, split,
+                                  stats_part)
         # eval: fold running statistics; one elementwise pass.
         scale = self.weight.float() * torch.rsqrt(self.running_var + self.eps)
         shift = self.bias.float() - self.running_mean * scale

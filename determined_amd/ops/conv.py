@@ -1,9 +1,22 @@
-"""ResNet stem convolution (3 -> 64, 7x7, stride 2, pad 3) on the CDNA4 kernels of
-csrc/conv_stem.hip: bf16 channels-last forward and weight gradient with the image rows staged
-once per output row in LDS (channel dim padded 3 -> 4 so every im2col operand is one aligned
-16-byte LDS read).  Anything else -- other shapes, fp32 inputs, an input that needs a gradient
--- runs the module's own convolution (MIOpen).
+"""Convolutions on the CDNA4 kernels.
+
+* ResNet stem (3 -> 64, 7x7, stride 2, pad 3): csrc/conv_stem.hip, bf16 channels-last forward
+  and weight gradient with the image rows staged once per output row in LDS (channel dim padded
+  3 -> 4 so every im2col operand is one aligned 16-byte LDS read).
+* Every other convolution with C, K multiples of 64 (all of ResNet-50's bottleneck convs):
+  csrc/conv_igemm.hip implicit GEMM -- the forward (with the following BatchNorm's batch
+  statistics emitted from the epilogue, so BN skips its statistics pass) and the stride-1 input
+  gradient (forward conv of dY with the flipped, transposed weights).  The weight gradient and
+  the strided input gradient stay on MIOpen.  Tile configurations are picked per layer shape by
+  timing every candidate once (MIOpen / hipBLASLt included for the input gradient), like
+  MIOpen's own find step.
+
+Anything else -- other shapes, fp32 inputs, modules with hooks or parametrizations -- runs the
+module's own convolution (MIOpen).
 """
+
+import os
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 from torch import nn
@@ -63,54 +76,148 @@ def stem_conv2d(conv: nn.Conv2d, x: torch.Tensor, with_stats: bool = False):
     return (y, None) if with_stats else y
 
 
-class _Conv1x1Fn(torch.autograd.Function):
-    """1x1 stride-1 convolution whose input gradient is one GEMM.  A channels-last activation is
-    an [N*H*W, C] row-major matrix, so dX = dY @ W on hipBLASLt writes dX directly, where
-    MIOpen's solvers zero-fill dX and then run a CK/igemm kernel.  The forward and the weight
-    gradient stay on MIOpen (dW as dY^T @ X has K = N*H*W and is 2-15x slower as a GEMM; the
-    forward as X @ W^T wins only on the channel-reducing 14x14/7x7 layers, ~0.15 ms/step total).
-    Measured per shape at batch 512: profiles/conv1x1_gemm_ab_b512_1gpu.jsonl,
-    profiles/conv1x1_fwd_gemm_ab_b512_1gpu.jsonl."""
+def _plain_module(conv: nn.Module) -> bool:
+    """No forward hooks / pre-hooks / parametrizations: calling the kernels directly instead of
+    ``conv(x)`` would silently skip them."""
+    return not (conv._forward_hooks or conv._forward_pre_hooks or hasattr(conv, "parametrizations"))
+
+
+# ---------------------------------------------------------------------------------------- autotune
+# key -> chosen candidate.  Candidates are ints (conv_igemm.hip tile configs) or strings
+# ("miopen", "gemm").  DAMD_CONV_TUNE=0 uses the static defaults instead of timing.
+_TUNE: Dict[tuple, object] = {}
+_TUNE_ON = os.environ.get("DAMD_CONV_TUNE", "1") != "0"
+
+
+def _time_once(fn: Callable[[], object], reps: int = 3) -> float:
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> object:
+    got = _TUNE.get(key)
+    if got is not None:
+        return got
+    if not _TUNE_ON or len(cands) <= 1 or torch.cuda.is_current_stream_capturing():
+        choice = default if default in cands else next(iter(cands))
+    else:
+        times = {c: _time_once(fn) for c, fn in cands.items()}
+        choice = min(times, key=times.get)
+    _TUNE[key] = choice
+    return choice
+
+
+def tuned_choices() -> Dict[tuple, object]:
+    """The per-shape kernel choices made so far (for reports / tests)."""
+    return dict(_TUNE)
+
+
+def _igemm_cfgs(ext, x: torch.Tensor, w: torch.Tensor):
+    return [c for c in range(ext.conv_num_cfgs()) if ext.conv_supported(x, w, c)]
+
+
+def _flip_weight(w: torch.Tensor) -> torch.Tensor:
+    """[K, C, R, S] -> [C, K, R, S] rotated by 180 degrees: the stride-1 input gradient is the
+    forward convolution of dY with these weights (padding R - 1 - pad)."""
+    return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    from determined_amd import ops
+
+    e = ops.ext()
+
+    def miopen():
+        return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                   [0, 0], 1, [True, False, False])[0]
+
+    k = w.shape[2]
+    if stride != 1 or 2 * pad != k - 1:
+        return miopen()
+    wt = _flip_weight(w)
+    cands: Dict[object, Callable[[], object]] = {}
+    for c in _igemm_cfgs(e, dy, wt):
+        cands[c] = (lambda c=c: e.conv_fwd(dy, wt, 1, k - 1 - pad, False, c, 0)[0])
+    cands["miopen"] = miopen
+    if k == 1:
+        n, cout, h, wd = dy.shape
+        cin = w.shape[1]
+
+        def gemm():
+            d2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            return (d2 @ w.reshape(cout, cin)).view(n, h, wd, cin).permute(0, 3, 1, 2)
+        cands["gemm"] = gemm
+    key = ("dgrad", tuple(dy.shape), tuple(w.shape), stride, pad)
+    return cands[_pick(key, cands, default=next(iter(cands)))]()
+
+
+class _IGemmConvFn(torch.autograd.Function):
+    """Forward on conv_igemm.hip (+ BN statistic partials); backward: input gradient by
+    :func:`_dgrad`, weight gradient on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight):
-        ctx.save_for_backward(x, weight)
-        return torch.nn.functional.conv2d(x, weight)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        n, cout, h, w = dy.shape
-        cin = x.shape[1]
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
-            dx = (dy2 @ weight.view(cout, cin)).view(n, h, w, cin).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
-        return dx, dw
-
-
-def conv1x1_gemm_wins(hw: int, cin: int, cout: int) -> bool:
-    """Shapes where the GEMM input gradient beat MIOpen on MI355X at batch 512
-    (profiles/conv1x1_gemm_ab_b512_1gpu.jsonl): every 14x14 / 7x7 layer, and the channel-reducing
-    layers at 56x56 / 28x28."""
-    return hw <= 14 or cin > cout
-
-
-def conv1x1(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """``conv(x)`` for a bias-free 1x1 stride-1 convolution; bf16 channels-last inputs on the GPU
-    take :class:`_Conv1x1Fn` where its GEMM input gradient is faster (``DAMD_DISABLE_FUSIONS=
-    conv1x1_gemm`` turns it off)."""
-    if (x.is_cuda and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16 and x.dim() == 4
-            and conv.bias is None and conv.groups == 1 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
-            and conv.padding == (0, 0) and conv.dilation == (1, 1) and x.requires_grad
-            and x.is_contiguous(memory_format=torch.channels_last) and torch.is_grad_enabled()
-            and conv1x1_gemm_wins(x.shape[2], conv.in_channels, conv.out_channels)):
+    def forward(ctx, x, weight, stride, pad, want_stats, cfg):
         from determined_amd import ops
 
-        if ops.fusion_enabled("conv1x1_gemm"):
-            return _Conv1x1Fn.apply(x, conv.weight)
-    return conv(x)
+        y, part = ops.ext().conv_fwd(x, weight, stride, pad, want_stats, cfg, 0)
+        ctx.save_for_backward(x, weight)
+        ctx.geo = (stride, pad)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart=None):
+        x, weight = ctx.saved_tensors
+        stride, pad = ctx.geo
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, x, weight, stride, pad)
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                     [0, 0], 1, [False, True, False])[1]
+        return dx, dw, None, None, None, None
+
+
+def igemm_fusable(conv: nn.Module, x: torch.Tensor) -> bool:
+    if not (isinstance(conv, nn.Conv2d) and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and conv.weight.dtype == torch.bfloat16 and conv.bias is None and conv.groups == 1
+            and conv.dilation == (1, 1) and conv.padding_mode == "zeros" and isinstance(conv.padding, tuple)
+            and conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
+            and conv.padding[0] == conv.padding[1] and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and _plain_module(conv)):
+        return False
+    from determined_amd import ops
+
+    return ops.fusion_enabled("igemm_conv") and bool(ops.ext().conv_supported(x, conv.weight, -1))
+
+
+def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """``(conv(x), stats_part)``: on the implicit-GEMM kernels when :func:`igemm_fusable`,
+    ``stats_part`` holding the per-channel (sum, sum of squares) partials of the output for the
+    following BatchNorm (``BatchNormAct2d.forward(y, stats_part=part)``); otherwise the module's
+    own convolution and ``None``."""
+    if not igemm_fusable(conv, x):
+        return conv(x), None
+    from determined_amd import ops
+
+    e = ops.ext()
+    st, pad = conv.stride[0], conv.padding[0]
+    w = conv.weight
+    key = ("fwd", tuple(x.shape), tuple(w.shape), st, pad)
+    cands = {c: (lambda c=c: e.conv_fwd(x, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, x, w)}
+    cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
+    stats = stats and ops.fusion_enabled("conv_stats")
+    y, part = _IGemmConvFn.apply(x, w, st, pad, stats, cfg)
+    return y, (part if stats else None)
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """``conv(x)`` on the implicit-GEMM kernels where supported (no statistics epilogue)."""
+    return conv_bn_input(conv, x, stats=False)[0]

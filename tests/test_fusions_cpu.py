@@ -67,17 +67,47 @@ def test_linear_gelu_fallback_matches_composition():
 
 def test_disable_fusions_env_switch():
     code = ("import determined_amd.ops as o; "
-            "print(o.fusion_enabled('split_grad'), o.fusion_enabled('stem_conv'), o.fusion_enabled('avgpool'))")
-    env = dict(os.environ, PYTHONPATH=ROOT, DAMD_DISABLE_FUSIONS="split_grad, stem_conv")
+            "print(o.fusion_enabled('split_grad'), o.fusion_enabled('stem_conv'), o.fusion_enabled('avgpool'), "
+            "o.fusion_enabled('igemm_conv'), o.fusion_enabled('conv_stats'))")
+    env = dict(os.environ, PYTHONPATH=ROOT, DAMD_DISABLE_FUSIONS="split_grad, stem_conv,igemm_conv")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
-    assert out.stdout.split() == ["False", "False", "True"]
+    assert out.stdout.split() == ["False", "False", "True", "False", "True"]
 
 
-def test_conv1x1_gemm_path_falls_back_on_cpu():
-    from determined_amd.ops.conv import conv1x1, conv1x1_gemm_wins
+def test_igemm_conv_path_falls_back_on_cpu():
+    from determined_amd.ops.conv import conv2d, conv_bn_input, igemm_fusable
 
-    conv = torch.nn.Conv2d(32, 16, 1, bias=False)
-    x = torch.randn(2, 32, 7, 7, requires_grad=True)
-    torch.testing.assert_close(conv1x1(conv, x), conv(x))
-    assert conv1x1_gemm_wins(14, 64, 256) and conv1x1_gemm_wins(56, 256, 64)
-    assert not conv1x1_gemm_wins(56, 64, 256) and not conv1x1_gemm_wins(28, 128, 512)
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False)
+    x = torch.randn(2, 64, 7, 7, requires_grad=True)
+    assert not igemm_fusable(conv, x)
+    y, part = conv_bn_input(conv, x)
+    assert part is None
+    torch.testing.assert_close(y, conv(x))
+    torch.testing.assert_close(conv2d(conv, x), conv(x))
+
+
+def test_igemm_conv_skips_modules_with_hooks():
+    from determined_amd.ops.conv import _plain_module
+
+    conv = torch.nn.Conv2d(64, 64, 1, bias=False)
+    assert _plain_module(conv)
+    h = conv.register_forward_hook(lambda m, i, o: None)
+    assert not _plain_module(conv)
+    h.remove()
+    conv.register_forward_pre_hook(lambda m, i: None)
+    assert not _plain_module(conv)
+    wn = torch.nn.utils.parametrizations.weight_norm(torch.nn.Conv2d(64, 64, 1, bias=False))
+    assert not _plain_module(wn)
+
+
+def test_resnet_forward_with_stats_path_matches_plain_on_cpu():
+    """The block forwards thread (y, stats_part) through conv_bn_input; on CPU the parts are None
+    and the result equals the module composition."""
+    from determined_amd.models.resnet import resnet18
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).train()
+    x = torch.randn(2, 3, 32, 32)
+    out = m(x)
+    assert out.shape == (2, 10) and torch.isfinite(out).all()
