@@ -61,6 +61,11 @@ extern "C" int damd_conv_num_cfgs();
 extern "C" int damd_conv_default_cfg(int, int64_t);
 extern "C" int damd_conv_supported(int, int, int);
 extern "C" int damd_conv_groups(int64_t, int, int, int);
+extern "C" int damd_wgrad_num_cfgs();
+extern "C" int damd_wgrad_supported(int, int, int);
+extern "C" int damd_wgrad_splits(int64_t, int, int, int, int, int, int);
+extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int, int,
+                                 int, int, int, hipStream_t);
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t);
 // launchers (bn.hip)
@@ -667,6 +672,37 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   return {y, part};
 }
 
+// dW of the convolution y = conv(x, w) (stride, pad) from dY, in w's dtype, as a channels-last
+// [K, C, R, S] tensor (physically [K][R][S][C]).
+bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t K, int64_t cfg) {
+  return x.is_cuda() && x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+         dy.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+         dy.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 && dy.size(1) == K &&
+         damd_wgrad_supported(static_cast<int>(x.size(1)), static_cast<int>(K), static_cast<int>(cfg));
+}
+
+at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t pad,
+                      int64_t cfg, int64_t splits) {
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t K = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(wgrad_supported(x, dy, K, cfg) && w.size(1) == C, "conv_wgrad: unsupported input / config");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat, "conv_wgrad: weight dtype");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == OH && dy.size(3) == OW, "conv_wgrad: dy shape");
+  const int64_t M = N * OH * OW;
+  const int sp = damd_wgrad_splits(M, static_cast<int>(C), static_cast<int>(K), static_cast<int>(R), static_cast<int>(S),
+                                   static_cast<int>(cfg), static_cast<int>(splits));
+  auto part = at::empty({sp, K * R * S * C}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({K, C, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = damd_wgrad_launch(x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), dtype_code(w),
+                                   static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                   static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
+                                   static_cast<int>(pad), static_cast<int>(cfg), sp, cur_stream());
+  TORCH_CHECK(rc == 0, "conv_wgrad: launch rejected");
+  return dw;
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -842,6 +878,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_supported", &conv_supported);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
+  m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
+  m.def("wgrad_supported", &wgrad_supported);
+  m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_default_cfg", [](int64_t K) { return damd_conv_default_cfg(static_cast<int>(K), 0); });
   m.def("stem_conv_supported", &stem_conv_supported);
   m.def("stem_conv_fwd", &stem_conv_fwd);

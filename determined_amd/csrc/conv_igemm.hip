@@ -71,6 +71,15 @@ __device__ __forceinline__ int a_row(int i, int rho) {
   return 32 * (i >> 1) + 8 * (rho >> 2) + 4 * (i & 1) + (rho & 3);
 }
 
+// n / d for 0 <= n < 2^31 by multiply-high (d fixed per launch, magic built on the host)
+struct FastDiv {
+  uint32_t d, mul, shift;
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> shift; }
+};
+
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
+
 template <int BCO, int BP, int WCO, bool STATS>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
@@ -271,6 +280,173 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   }
 }
 
+
+// =============================================================================== weight gradient
+// dW[co][k] = sum_p dY[p][co] . im2col[p][k], k = (r, s, c): rows co, columns k, reduction over
+// the output pixels p (the MFMA K dimension).  Both operands are pixel-major in memory, so the
+// LDS images keep pixel rows ([64 px][64 ch] blocks, 128-byte rows, filled by the same LDS-DMA
+// gather as the forward) and the fragments are read with the hardware transpose
+// ds_read_b64_tr_b16: lane c of a 16-lane group receives channel col0 + c of 4 pixel rows.
+// Swizzle for these reads: chunk c of row r at slot c ^ (2 * ((r >> 1) & 3)) -- conflict-free per
+// 32-lane half for the 4-row x 32-byte blocks the transposed reads take.
+// Fragment k-order: elements 0..3 = pixels r0..r0+3, 4..7 = r0+16..r0+19 (r0 = 32 kk + 4 g) for
+// both operands, so the permuted pixel order cancels in the product.
+// The pixel range is split over `splits` blocks per output tile; each block writes an fp32 partial
+// tile and wgrad_finalize_kernel sums the splits in a fixed order (deterministic).
+
+__device__ __forceinline__ int swz_tr(int row) { return 2 * ((row >> 1) & 3); }
+
+struct WGeo {
+  int H, W, C, OH, OW, K, R, S, stride, pad;
+  int M;          // pixels (output positions)
+  int cotiles, ktiles, splits, chunk;  // chunk: pixels per split (multiple of 64)
+  int kblk_per_tap;                    // C / BKC
+  FastDiv dOHW, dOW;
+};
+
+template <int BCO, int BKC, int WCO>
+__global__ void __launch_bounds__(kThreads, 2)
+conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part, WGeo g) {
+  constexpr int WK = 4 / WCO;
+  constexpr int TCO = BCO / WCO, TK = BKC / WK;
+  constexpr int FI = TCO / 16, FJ = TK / 16;
+  static_assert(WCO * WK == 4 && FI >= 1 && FJ >= 1 && BCO % 64 == 0 && BKC % 64 == 0, "bad tile");
+  constexpr int ACB = BCO / 64, BCB = BKC / 64;   // 64-channel blocks per operand
+  constexpr int BLK = 64 * 64;                    // elements per [64 px][64 ch] block
+  constexpr int STAGE = (ACB + BCB) * BLK;
+  constexpr int NI = (ACB + BCB) * 8 / 4;         // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c16 = lane & 15, lg = lane >> 4;
+  const int wco0 = (wave % WCO) * TCO, wk0 = (wave / WCO) * TK;
+
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ntile = g.cotiles * g.ktiles;
+  const int tile = rid % ntile, split = rid / ntile;
+  const int cot = tile % g.cotiles, kt = tile / g.cotiles;
+  const int tap = kt / g.kblk_per_tap;
+  const int ci0 = (kt - tap * g.kblk_per_tap) * BKC;
+  const int tr = tap / g.S, ts = tap - (tap / g.S) * g.S;
+  const int p_begin = split * g.chunk;
+  int p_end = p_begin + g.chunk;
+  if (p_end > g.M) p_end = g.M;
+  const int items = p_end > p_begin ? (p_end - p_begin + 63) / 64 : 0;
+  const bool plain = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+
+  const int prow = lane >> 3, slot = lane & 7;
+  auto issue = [&](int stage, int it) {
+    bf16_t* base = lds + stage * STAGE;
+    const int p0 = p_begin + it * 64;
+#pragma unroll
+    for (int n = 0; n < NI; ++n) {
+      const int ins = wave + 4 * n;               // 0 .. (ACB+BCB)*8-1
+      const int blk = ins >> 3, row = 8 * (ins & 7) + prow;
+      const int p = p0 + row;
+      const int chunk = slot ^ swz_tr(row);
+      const bf16_t* src = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+      if (p < p_end) {
+        if (blk < ACB) {
+          src = dy + static_cast<int64_t>(p) * g.K + cot * BCO + blk * 64 + (chunk << 3);
+        } else if (plain) {
+          src = x + static_cast<int64_t>(p) * g.C + ci0 + (blk - ACB) * 64 + (chunk << 3);
+        } else {
+          const int nimg = static_cast<int>(g.dOHW.div(static_cast<uint32_t>(p)));
+          const int rem = p - nimg * g.OH * g.OW;
+          const int oh = static_cast<int>(g.dOW.div(static_cast<uint32_t>(rem)));
+          const int ow = rem - oh * g.OW;
+          const int ih = oh * g.stride - g.pad + tr, iw = ow * g.stride - g.pad + ts;
+          if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) && static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
+            src = x + ((static_cast<int64_t>(nimg) * g.H + ih) * g.W + iw) * g.C + ci0 + (blk - ACB) * 64 + (chunk << 3);
+        }
+      }
+      dma16(src, base + blk * BLK + 8 * (ins & 7) * 64);
+    }
+  };
+
+  // transposed fragment: channels col0..col0+15 (lane c16 -> col0 + c16) of pixel rows r0..r0+3
+  // and r0+16..r0+19 of a [64 px][64 ch] block image
+  auto tr_frag = [&](const bf16_t* blkimg, int col0, int r0) {
+    const int q = c16 >> 2, pp = c16 & 3;
+    const int col = col0 + 4 * pp, chunk = col >> 3, within = col & 7;
+    const int ra = r0 + q, rb = r0 + 16 + q;
+    const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(blkimg + ra * 64 + ((chunk ^ swz_tr(ra)) << 3) + within));
+    const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(blkimg + rb * 64 + ((chunk ^ swz_tr(rb)) << 3) + within));
+    s8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  };
+
+  f4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (items > 0) issue(0, 0);
+  for (int it = 0; it < items; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (it + 1 < items) issue((it + 1) & 1, it + 1);
+    const bf16_t* sa = lds + (it & 1) * STAGE;
+    const bf16_t* sb = sa + ACB * BLK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = 32 * kk + 4 * lg;
+      s8 a[FI], b[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int col = wco0 + 16 * i;
+        a[i] = tr_frag(sa + (col >> 6) * BLK, col & 63, r0);
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int col = wk0 + 16 * j;
+        b[j] = tr_frag(sb + (col >> 6) * BLK, col & 63, r0);
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+  }
+  // acc[i][j][r] = partial dW[co = cot*BCO + wco0 + 16i + 4lg + r][k = kt*BKC + wk0 + 16j + c16]
+  const int64_t Ktot = static_cast<int64_t>(g.R) * g.S * g.C;
+  float* dst = part + static_cast<int64_t>(split) * g.K * Ktot;
+  const int64_t kcol0 = static_cast<int64_t>(tap) * g.C + ci0 + wk0;
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t co = static_cast<int64_t>(cot) * BCO + wco0 + 16 * i + 4 * lg + r;
+        dst[co * Ktot + kcol0 + 16 * j + c16] = acc[i][j][r];
+      }
+}
+
+// dW = sum over splits (fixed order) of part[split][n], 4 consecutive outputs per thread.
+template <typename WT>
+__global__ void __launch_bounds__(256)
+wgrad_finalize_kernel(const float* __restrict__ part, int splits, int64_t n, WT* __restrict__ dw) {
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 s = *reinterpret_cast<const float4*>(part + i);
+  for (int k = 1; k < splits; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  Elem<WT>::st(dw, i, s.x);
+  Elem<WT>::st(dw, i + 1, s.y);
+  Elem<WT>::st(dw, i + 2, s.z);
+  Elem<WT>::st(dw, i + 3, s.w);
+}
+
 // Per-config resources: LDS bytes per block (for the residency estimate).
 template <int BCO, int BP>
 constexpr int lds_bytes() { return 2 * (BCO + BP) * kBK * 2; }
@@ -360,6 +536,82 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
     default: L(256, 128, 4); break;
   }
 #undef L
+  DAMD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+// ---- weight gradient
+namespace {
+FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t mul = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{d, static_cast<uint32_t>(mul), l};
+}
+struct WCfg {
+  int bco, bkc, wco;
+};
+// 0: 128x128 (2x2 waves), 1: 64x128 (1x4), 2: 128x64 (4x1), 3: 64x64 (2x2: 32x32 per wave)
+constexpr WCfg kWCfgs[] = {{128, 128, 2}, {64, 128, 1}, {128, 64, 4}, {64, 64, 2}};
+constexpr int kNumWCfgs = sizeof(kWCfgs) / sizeof(kWCfgs[0]);
+}  // namespace
+
+extern "C" {
+
+int damd_wgrad_num_cfgs() { return kNumWCfgs; }
+
+int damd_wgrad_supported(int C, int K, int cfg) {
+  if (cfg < 0 || cfg >= kNumWCfgs) return 0;
+  return C % kWCfgs[cfg].bkc == 0 && K % kWCfgs[cfg].bco == 0;
+}
+
+// number of pixel splits (leading dim of the fp32 partials)
+int damd_wgrad_splits(int64_t M, int C, int K, int R, int S, int cfg, int splits_override) {
+  const WCfg c = kWCfgs[cfg];
+  const int64_t tiles = static_cast<int64_t>(K / c.bco) * (R * S * C / c.bkc);
+  int64_t splits = splits_override > 0 ? splits_override : (512 + tiles - 1) / tiles;
+  const int64_t max_splits = (M + 255) / 256;  // at least 4 k-steps per block
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  return static_cast<int>(splits);
+}
+
+// x: [N, H, W, C]; dy: [N, OH, OW, K]; part: [splits][K][R*S*C] fp32 scratch; dw: [K][R][S][C]
+int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int w_dtype, int N, int H, int W, int C,
+                      int K, int R, int S, int stride, int pad, int cfg, int splits, hipStream_t st) {
+  if (!damd_wgrad_supported(C, K, cfg)) return -1;
+  const WCfg c = kWCfgs[cfg];
+  WGeo g;
+  g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
+  g.OH = (H + 2 * pad - R) / stride + 1;
+  g.OW = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = static_cast<int64_t>(N) * g.OH * g.OW;
+  if (M >= (int64_t{1} << 31) - 4096) return -2;
+  g.M = static_cast<int>(M);
+  g.cotiles = K / c.bco;
+  g.kblk_per_tap = C / c.bkc;
+  g.ktiles = R * S * g.kblk_per_tap;
+  g.splits = splits;
+  g.chunk = static_cast<int>(((M + splits - 1) / splits + 63) / 64 * 64);
+  g.dOHW = make_fastdiv(static_cast<uint32_t>(g.OH * g.OW));
+  g.dOW = make_fastdiv(static_cast<uint32_t>(g.OW));
+  const dim3 grid(static_cast<unsigned>(g.cotiles * g.ktiles * splits));
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* dp = static_cast<const bf16_t*>(dy);
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
+    case 1: hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
+    case 2: hipLaunchKernelGGL((conv_wgrad_kernel<128, 64, 4>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
+    default: hipLaunchKernelGGL((conv_wgrad_kernel<64, 64, 2>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
+  }
+  const int64_t n = static_cast<int64_t>(K) * R * S * C;  // multiple of 4 (C % 64 == 0)
+  const dim3 fg(static_cast<unsigned>((n / 4 + 255) / 256));
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
+  else
+    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
   return 0;
 }

@@ -6,10 +6,11 @@
 * Every other convolution with C, K multiples of 64 (all of ResNet-50's bottleneck convs):
   csrc/conv_igemm.hip implicit GEMM -- the forward (with the following BatchNorm's batch
   statistics emitted from the epilogue, so BN skips its statistics pass) and the stride-1 input
-  gradient (forward conv of dY with the flipped, transposed weights).  The weight gradient and
-  the strided input gradient stay on MIOpen.  Tile configurations are picked per layer shape by
-  timing every candidate once (MIOpen / hipBLASLt included for the input gradient), like
-  MIOpen's own find step.
+  gradient (forward conv of dY with the flipped, transposed weights), and the weight gradient
+  (pixel-split MFMA kernel with transposed LDS reads + deterministic split reduction).  The
+  strided input gradient stays on MIOpen.  Tile configurations are picked per layer shape by
+  timing every candidate once (MIOpen / hipBLASLt included for the gradients), like MIOpen's own
+  find step.
 
 Anything else -- other shapes, fp32 inputs, modules with hooks or parametrizations -- runs the
 module's own convolution (MIOpen).
@@ -157,6 +158,26 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
     return cands[_pick(key, cands, default=next(iter(cands)))]()
 
 
+def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    """Weight gradient: conv_igemm.hip's split-pixel kernel or MIOpen, whichever timed faster for
+    this shape."""
+    from determined_amd import ops
+
+    e = ops.ext()
+
+    def miopen():
+        return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                   [0, 0], 1, [False, True, False])[1]
+
+    cands: Dict[object, Callable[[], object]] = {}
+    for c in range(e.wgrad_num_cfgs()):
+        if e.wgrad_supported(x, dy, w.shape[0], c):
+            cands[c] = (lambda c=c: e.conv_wgrad(x, dy, w, stride, pad, c, 0))
+    cands["miopen"] = miopen
+    key = ("wgrad", tuple(x.shape), tuple(w.shape), stride, pad)
+    return cands[_pick(key, cands, default="miopen")]()
+
+
 class _IGemmConvFn(torch.autograd.Function):
     """Forward on conv_igemm.hip (+ BN statistic partials); backward: input gradient by
     :func:`_dgrad`, weight gradient on MIOpen."""
@@ -180,8 +201,7 @@ class _IGemmConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, x, weight, stride, pad)
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False,
-                                                     [0, 0], 1, [False, True, False])[1]
+            dw = _wgrad(dy, x, weight, stride, pad)
         return dx, dw, None, None, None, None
 
 

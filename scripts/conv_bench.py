@@ -64,7 +64,8 @@ def main():
     dev = torch.device("cuda")
     out = open(a.out, "a") if a.out else None
     idx = [int(i) for i in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
-    tot = {"miopen_fwd": 0.0, "ours_fwd": 0.0, "miopen_dgrad": 0.0, "ours_dgrad": 0.0}
+    tot = {"miopen_fwd": 0.0, "ours_fwd": 0.0, "miopen_dgrad": 0.0, "ours_dgrad": 0.0, "miopen_wgrad": 0.0,
+           "ours_wgrad": 0.0}
     for si in idx:
         cin, cout, k, st, hw, cnt = SHAPES[si]
         pad = k // 2
@@ -118,6 +119,25 @@ def main():
             if rec["ours_dgrad_us"]:
                 tot["miopen_dgrad"] += rec["miopen_dgrad_us"] * cnt
                 tot["ours_dgrad"] += min(min(rec["ours_dgrad_us"].values()), rec["miopen_dgrad_us"]) * cnt
+        if a.only in ("", "wgrad"):
+            dyw = cl(torch.randn(a.batch, cout, oh, oh, device=dev).to(torch.bfloat16))
+
+            def miopen_wgrad():
+                return torch.ops.aten.convolution_backward(dyw, x, w, None, [st, st], [pad, pad], [1, 1], False,
+                                                           [0, 0], 1, [False, True, False])[1]
+            rec["miopen_wgrad_us"] = round(timeit(miopen_wgrad), 1)
+            dys = cl(torch.randn(3, cout, oh, oh, device=dev).to(torch.bfloat16))
+            refw = torch.nn.grad.conv2d_weight(xs.float(), w.shape, dys.float(), stride=st, padding=pad)
+            rec["ours_wgrad_us"] = {}
+            rec["wgrad_err"] = {}
+            for cfg in range(e.wgrad_num_cfgs()):
+                if e.wgrad_supported(x, dyw, cout, cfg):
+                    got = e.conv_wgrad(xs, dys, w, st, pad, cfg, 0).float()
+                    rec["wgrad_err"][str(cfg)] = round(((got - refw).norm() / refw.norm()).item(), 5)
+                    rec["ours_wgrad_us"][str(cfg)] = round(timeit(lambda: e.conv_wgrad(x, dyw, w, st, pad, cfg, 0)), 1)
+            if rec["ours_wgrad_us"]:
+                tot["miopen_wgrad"] += rec["miopen_wgrad_us"] * cnt
+                tot["ours_wgrad"] += min(min(rec["ours_wgrad_us"].values()), rec["miopen_wgrad_us"]) * cnt
         line = json.dumps(rec)
         print(line, flush=True)
         if out:

@@ -7,6 +7,8 @@ import sys
 def cat(n: str) -> str:
     if "damd::bn_" in n:
         return "bn(ours)"
+    if "damd::igemm" in n or "damd::stem" in n:
+        return "conv(ours)"
     if "damd::" in n:
         return "optim/norm(ours)"
     if "batch_norm" in n:

@@ -64,3 +64,29 @@ def test_conv_dgrad_via_flipped_weights(ext, shape):
         pytest.skip("channel count not covered by a config")
     dx, _ = ext.conv_fwd(dy, wt, 1, k - 1 - pad, False, -1, 0)
     torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", SHAPES + [(2, 64, 128, 3, 1, 23), (1, 128, 64, 1, 1, 40)])
+def test_conv_wgrad_matches_fp32(ext, shape):
+    n, cin, cout, k, st, hw = shape
+    pad = k // 2
+    torch.manual_seed(2)
+    x = cl(torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16))
+    w = cl(torch.randn(cout, cin, k, k, device="cuda").to(torch.bfloat16))
+    oh = (hw + 2 * pad - k) // st + 1
+    dy = cl(torch.randn(n, cout, oh, oh, device="cuda").to(torch.bfloat16))
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), stride=st, padding=pad)
+    ran = 0
+    for cfg in range(ext.wgrad_num_cfgs()):
+        if not ext.wgrad_supported(x, dy, cout, cfg):
+            continue
+        for splits in (0, 1, 3):
+            dw = ext.conv_wgrad(x, dy, w, st, pad, cfg, splits)
+            assert dw.shape == w.shape and dw.dtype == w.dtype
+            torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        ran += 1
+    assert ran > 0
+    cfg0 = 0 if ext.wgrad_supported(x, dy, cout, 0) else 3
+    dw32 = ext.conv_wgrad(x, dy, w.float(), st, pad, cfg0, 0)
+    assert dw32.dtype == torch.float32
+    torch.testing.assert_close(dw32, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
