@@ -67,11 +67,14 @@ extern "C" int damd_wgrad_splits(int64_t, int, int, int, int, int, int);
 extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int, int,
                                  int, int, int, hipStream_t);
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
-                                    int, int, int, hipStream_t);
+                                    int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
+                                    const float*, const float*, const float*);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
                         float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*, const float*, int);
+void damd_bn_bwd_from_part_launch(const void*, const void*, int64_t, int, const float*, const float*, const float*,
+                                  const float*, int, float*, void*, void*, void*, int, int, hipStream_t);
 void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
                                hipStream_t);
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
@@ -441,6 +444,27 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// BN backward from producer-computed reduce partials (conv_dgrad_bn): dz already carries the
+// ReLU mask; returns (dx, dgamma, dbeta).
+std::vector<at::Tensor> bn_bwd_from_part(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& stats,
+                                         const at::Tensor& weight, const at::Tensor& part) {
+  check_bn_tensor(dz, x, "dz");
+  TORCH_CHECK(bn_supported(x), "bn_bwd_from_part: unsupported x");
+  const int64_t C = bn_channels(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 3 && part.size(1) == 2 && part.size(2) == C &&
+              part.is_contiguous(), "bn_bwd_from_part: part must be float32 [nb, 2, C]");
+  auto coef = at::empty({3, C}, x.options().dtype(at::kFloat));
+  auto dgamma = at::empty({C}, weight.options());
+  auto dbeta = at::empty({C}, weight.options());
+  auto dx = at::empty_like(x);
+  damd_bn_bwd_from_part_launch(dz.data_ptr(), x.data_ptr(), M, static_cast<int>(C), stats[0].data_ptr<float>(),
+                               stats[1].data_ptr<float>(), stats[2].data_ptr<float>(), part.data_ptr<float>(),
+                               static_cast<int>(part.size(0)), coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(),
+                               dx.data_ptr(), dtype_code(x), dtype_code(weight), cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
 // ---------------------------------------------------------------- residual add + dropout + LayerNorm
 bool resid_norm_supported(const at::Tensor& x) {
   return x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
@@ -667,9 +691,57 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int rc = damd_conv_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
-                                      static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream());
+                                      static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
+                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
   return {y, part};
+}
+
+// Stride-1 input gradient dX = conv(dY, wt, pad) (wt = flipped, transposed weights) of a conv
+// whose input was a = relu(bn(yb) [+ residual]), with the BN backward's reduce fused into the
+// epilogue: returns (dz, part [groups, 2, C]) where dz = (dX [+ d2]) * [a > 0] (the gradient at
+// the BN's output; also the residual's gradient) and part = (sum dz, sum dz * (yb - mean)) for
+// the BN backward finalize.  mask: the forward's ReLU bit mask, or absent to recompute the ReLU
+// from yb * scale + shift (no residual).  stats: [4, C] (mean, invstd, scale, shift).
+std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt, int64_t pad, int64_t cfg,
+                                      const c10::optional<at::Tensor>& d2, const at::Tensor& yb,
+                                      const c10::optional<at::Tensor>& mask, const at::Tensor& stats) {
+  if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(wt.size(0)), 0);
+  TORCH_CHECK(conv_supported(dy, wt, cfg), "conv_dgrad_bn: unsupported input / weight / config");
+  const int64_t N = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
+  const int64_t K = wt.size(0), R = wt.size(2), S = wt.size(3);
+  TORCH_CHECK(R == S && 2 * pad == R - 1, "conv_dgrad_bn: stride-1 same-size convolutions only");
+  TORCH_CHECK(yb.scalar_type() == at::kBFloat16 && yb.dim() == 4 && yb.size(0) == N && yb.size(1) == K &&
+              yb.size(2) == H && yb.size(3) == W && yb.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_bn: yb must be the [N, K, H, W] channels-last bf16 BN input");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(0) == 4 && stats.size(1) == K &&
+              stats.is_contiguous(), "conv_dgrad_bn: stats must be float32 [4, K]");
+  const void* d2p = nullptr;
+  if (d2.has_value() && d2->defined()) {
+    TORCH_CHECK(d2->sizes() == yb.sizes() && d2->strides() == yb.strides() && d2->scalar_type() == at::kBFloat16,
+                "conv_dgrad_bn: d2 must match yb");
+    d2p = d2->data_ptr();
+  }
+  const uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined() && mask->numel() > 0) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() == yb.numel() / 8 && mask->is_contiguous(),
+                "conv_dgrad_bn: mask must be uint8 [numel / 8]");
+    mp = mask->data_ptr<uint8_t>();
+  }
+  const int64_t M = N * H * W;
+  TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_dgrad_bn: tensor too large");
+  auto wl = wt.contiguous(at::MemoryFormat::ChannelsLast);
+  auto dz = at::empty_like(yb);
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(cfg), 0);
+  auto part = at::empty({G, 2, K}, dy.options().dtype(at::kFloat));
+  const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
+                                      static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                      static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
+                                      static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
+                                      yb.data_ptr(), mp, stats[0].data_ptr<float>(), stats[2].data_ptr<float>(),
+                                      stats[3].data_ptr<float>());
+  TORCH_CHECK(rc == 0, "conv_dgrad_bn: launch rejected");
+  return {dz, part};
 }
 
 // dW of the convolution y = conv(x, w) (stride, pad) from dY, in w's dtype, as a channels-last
@@ -868,6 +940,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("bn_bwd_from_part", &bn_bwd_from_part);
   m.def("bn_apply", &bn_apply);
   m.def("bn_pool_fwd", &bn_pool_fwd);
   m.def("resid_norm_supported", &resid_norm_supported);
@@ -877,6 +950,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("global_avgpool_bwd", &global_avgpool_bwd);
   m.def("conv_supported", &conv_supported);
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
   m.def("wgrad_supported", &wgrad_supported);

@@ -80,17 +80,45 @@ struct FastDiv {
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4 lds_s4;
 
-template <int BCO, int BP, int WCO, bool STATS>
-__global__ void __launch_bounds__(kThreads, 2)
+// NW waves (64 * NW threads), NST-slot LDS ring: NST - 1 k-steps of DMA in flight ahead of the
+// MFMAs, retired by counted waits (vmcnt counts loads and stores together in issue order, so a
+// count of the younger DMA instructions is exact without epilogue stores and conservative with
+// them) and a raw s_barrier (a __syncthreads() fence would drain the whole ring).
+// Epilogue modes (EPI):
+//   kEpiNone  : store out
+//   kEpiStats : store out + (sum, sum sq) partials of the bf16 outputs (the next BN's statistics)
+//   kEpiBnbM / kEpiBnbR : the kernel is the input gradient of a conv whose input was
+//       a = relu(bn(yb) [+ residual]); it stores dz = (acc [+ d2]) * [a > 0] (the gradient at the
+//       BN output, ReLU mask from the forward's bit mask (M) or recomputed as
+//       yb*scale + shift > 0 (R)) and the partials (sum dz, sum dz*(yb - mean)) of that BN's
+//       backward -- the BN-backward reduce pass over (dz, yb) is never run.
+constexpr int kEpiNone = 0, kEpiStats = 1, kEpiBnbM = 2, kEpiBnbR = 3;
+
+struct EpiArgs {
+  const bf16_t* d2;      // second gradient of the BN output (shortcut consumer) or null
+  const bf16_t* yb;      // BN input, [M][K]
+  const uint8_t* mask;   // ReLU bit mask [M][K/8] (kEpiBnbM)
+  const float* mean;     // BN batch mean [K]
+  const float* scale;    // folded BN scale / shift [K] (kEpiBnbR)
+  const float* shift;
+};
+
+template <int BCO, int BP, int WCO, int NW, int NST, int EPI>
+__global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-                float* __restrict__ part, Geo g) {
-  constexpr int WP = 4 / WCO;
+                float* __restrict__ part, Geo g, EpiArgs ea) {
+  constexpr bool SUMS = EPI != kEpiNone;
+  constexpr int NT = 64 * NW;
+  constexpr int WP = NW / WCO;
   constexpr int TCO = BCO / WCO, TP = BP / WP;
   constexpr int FI = TCO / 16, FJ = TP / 16;
-  static_assert(WCO * WP == 4 && FI % 2 == 0 && FJ >= 1 && BCO % 32 == 0 && BP % 32 == 0, "bad tile");
+  static_assert(WCO * WP == NW && FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && BP % (8 * NW) == 0, "bad tile");
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
   constexpr int STAGE = (BCO + BP) * kBK;  // elements per stage
-  constexpr int NIW = BCO / 32, NIX = BP / 32;  // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  constexpr int NIW = BCO / (8 * NW), NIX = BP / (8 * NW);  // DMA instructions per wave per stage
+  constexpr int NL = NIW + NIX;
+  static_assert(NL * (NST - 2) <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE];
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rho = lane & 15, lg = lane >> 4;
@@ -110,7 +138,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   const bf16_t* wsrc[NIW];
 #pragma unroll
   for (int i = 0; i < NIW; ++i) {
-    const int co = 8 * (wave + 4 * i) + prow;
+    const int co = 8 * (wave + NW * i) + prow;
     wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
   }
   // pixel rows: per tile (image offset + chunk, top-left input coordinate, validity)
@@ -120,7 +148,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   auto tile_rows = [&](int pt) {
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
-      const int p = 8 * (wave + 4 * i) + prow;
+      const int p = 8 * (wave + NW * i) + prow;
       const int m = pt * BP + p;  // M < 2^31 (host-checked)
       if (m < g.M) {
         const int n = m / OHW;
@@ -144,7 +172,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     const int pt = grp + l_tile * g.groups;
     if (l_ks == 0) tile_rows(pt);
 #pragma unroll
-    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + 4 * i) * kBK);
+    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + NW * i) * kBK);
     const int c0 = l_cb * kBK;
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
@@ -153,7 +181,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
                       static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
       const bf16_t* src = ok ? x + xoff[i] + (static_cast<int64_t>(ih) * g.W + iw) * g.C + c0
                              : reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
-      dma16(src, sw + (BCO + 8 * (wave + 4 * i)) * kBK);
+      dma16(src, sw + (BCO + 8 * (wave + NW * i)) * kBK);
     }
     // advance (cb fastest, then s, then r, then tile)
     if (++l_cb == g.cblk) {
@@ -172,20 +200,26 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   float st_s[FI / 2][8], st_q[FI / 2][8];
-  if (STATS) {
+  if (SUMS) {
 #pragma unroll
     for (int q = 0; q < FI / 2; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
   }
 
-  if (items > 0) issue(0);
+#pragma unroll
+  for (int s0 = 0; s0 < NST - 1; ++s0)
+    if (s0 < items) issue(s0);
   int c_ks = 0, c_tile = 0;
   for (int it = 0; it < items; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage it&1 landed for every wave; stage (it+1)&1 is no longer read
-    if (it + 1 < items) issue((it + 1) & 1);
-    const bf16_t* sw = lds + (it & 1) * STAGE;
+    // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
+    const int ahead = items - 1 - it;
+    if (NST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
+    else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
+    if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+    const bf16_t* sw = lds + (it % NST) * STAGE;
     const bf16_t* sx = sw + BCO * kBK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -215,22 +249,59 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         const bool ok = m < g.M;
 #pragma unroll
         for (int q = 0; q < FI / 2; ++q) {
+          const int64_t co = static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
+          float yv[8];
+          if (EPI >= kEpiBnbM && ok) {
+            if (ea.d2 != nullptr) {
+              const bf16x8 dv = *reinterpret_cast<const bf16x8*>(ea.d2 + m * g.K + co);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o[e] += bf2f(dv.v[e]);
+            }
+            const bf16x8 yr = *reinterpret_cast<const bf16x8*>(ea.yb + m * g.K + co);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) yv[e] = bf2f(yr.v[e]);
+            if (EPI == kEpiBnbM) {
+              const uint32_t mb = ea.mask[(m * g.K + co) >> 3];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o[e] = (mb >> e) & 1u ? o[e] : 0.f;
+            } else {
+              const float4 s0 = *reinterpret_cast<const float4*>(ea.scale + co);
+              const float4 s1 = *reinterpret_cast<const float4*>(ea.scale + co + 4);
+              const float4 h0 = *reinterpret_cast<const float4*>(ea.shift + co);
+              const float4 h1 = *reinterpret_cast<const float4*>(ea.shift + co + 4);
+              const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+              const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o[e] = yv[e] * sc[e] + sh[e] > 0.f ? o[e] : 0.f;
+            }
+          }
           bf16x8 v;
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const u16v2_t p0 = f2bf2(acc[2 * q][j][e], acc[2 * q][j][e + 1]);
-            const u16v2_t p1 = f2bf2(acc[2 * q + 1][j][e], acc[2 * q + 1][j][e + 1]);
-            v.v[e] = p0[0]; v.v[e + 1] = p0[1];
-            v.v[4 + e] = p1[0]; v.v[5 + e] = p1[1];
+          for (int e = 0; e < 8; e += 2) {
+            const u16v2_t pk = f2bf2(o[e], o[e + 1]);
+            v.v[e] = pk[0]; v.v[e + 1] = pk[1];
           }
           if (ok) {
-            *reinterpret_cast<bf16x8*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg) = v;
-            if (STATS) {
+            *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
+            if (EPI == kEpiStats) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 const float f = bf2f(v.v[e]);
                 st_s[q][e] += f;
                 st_q[q][e] += f * f;
+              }
+            } else if (EPI >= kEpiBnbM) {
+              const float4 u0 = *reinterpret_cast<const float4*>(ea.mean + co);
+              const float4 u1 = *reinterpret_cast<const float4*>(ea.mean + co + 4);
+              const float mu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float f = bf2f(v.v[e]);  // the stored (rounded) dz, as the apply pass reads it
+                st_s[q][e] += f;
+                st_q[q][e] += f * (yv[e] - mu[e]);
               }
             }
           }
@@ -245,7 +316,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
   }
 
-  if (STATS) {
+  if (SUMS) {
     // sum over the 16 pixel lanes of each lane group, then over the WP waves sharing a co range
 #pragma unroll
     for (int q = 0; q < FI / 2; ++q)
@@ -270,7 +341,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < 2 * BCO; t += kThreads) {
+    for (int t = threadIdx.x; t < 2 * BCO; t += NT) {
       const int which = t / BCO, co = t - which * BCO;
       float s = 0.f;
 #pragma unroll
@@ -447,9 +518,6 @@ wgrad_finalize_kernel(const float* __restrict__ part, int splits, int64_t n, WT*
   Elem<WT>::st(dw, i + 3, s.w);
 }
 
-// Per-config resources: LDS bytes per block (for the residency estimate).
-template <int BCO, int BP>
-constexpr int lds_bytes() { return 2 * (BCO + BP) * kBK * 2; }
 
 }  // namespace igemm
 }  // namespace damd
@@ -460,16 +528,19 @@ using namespace damd::igemm;
 namespace {
 
 struct Cfg {
-  int bco, bp, wco;
+  int bco, bp, wco, nw, nst;
 };
-// cfg ids: 0: 64x128 (1x4 waves), 1: 128x128 (2x2), 2: 128x256 (2x2), 3: 64x256 (1x4), 4: 256x128 (4x1)
-constexpr Cfg kCfgs[] = {{64, 128, 1}, {128, 128, 2}, {128, 256, 2}, {64, 256, 1}, {256, 128, 4}};
+// 0-2: 4 waves, 2-slot ring; 3-5: 8 waves, 3-slot ring (the tiles that won on some ResNet-50
+// layer in profiles/conv_igemm_*; 128x256 / 256x128 with 4 waves spill and never won)
+constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2},  {128, 128, 2, 4, 2}, {64, 256, 1, 4, 2},
+                         {128, 256, 2, 8, 3}, {64, 256, 1, 8, 3},  {256, 128, 4, 8, 3}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-int blocks_per_cu(int bco, int bp) {
-  const int lds = 2 * (bco + bp) * kBK * 2;
+int blocks_per_cu(const Cfg& c) {
+  const int lds = c.nst * (c.bco + c.bp) * kBK * 2;
   int occ = (160 * 1024) / lds;
-  if (occ > 2) occ = 2;  // __launch_bounds__(256, 2)
+  const int by_waves = 8 / c.nw;  // __launch_bounds__(64 * NW, 2): <= 2 waves per SIMD
+  if (occ > by_waves) occ = by_waves;
   return occ < 1 ? 1 : occ;
 }
 
@@ -482,8 +553,9 @@ int damd_conv_num_cfgs() { return kNumCfgs; }
 // Heuristic default config for a layer: widest co tile the channel count allows.
 int damd_conv_default_cfg(int K, int64_t M) {
   (void)M;
+  if (K % 256 == 0) return 5;
   if (K % 128 == 0) return 1;
-  return 0;
+  return 2;
 }
 
 int damd_conv_supported(int C, int K, int cfg) {
@@ -497,17 +569,24 @@ int damd_conv_groups(int64_t M, int K, int cfg, int groups_override) {
   const int64_t ptiles = (M + c.bp - 1) / c.bp;
   const int ctiles = K / c.bco;
   int64_t groups = groups_override > 0 ? groups_override
-                                       : (256LL * blocks_per_cu(c.bco, c.bp) + ctiles - 1) / ctiles;
+                                       : (256LL * blocks_per_cu(c) + ctiles - 1) / ctiles;
   if (groups > ptiles) groups = ptiles;
   if (groups < 1) groups = 1;
   return static_cast<int>(groups);
 }
 
 // x: [N, H, W, C] bf16; w: [K, R, S, C] bf16; y: [N, OH, OW, K] bf16;
-// part: null or [groups][2][K] fp32 (sum, sum of squares of the bf16 outputs)
+// part: null or [groups][2][K] fp32 (epi 1: sum / sum of squares of y; epi 2, 3: see EpiArgs)
+// epi: 0 none, 1 stats, 2 BN-backward with bit mask, 3 BN-backward with recomputed ReLU mask
 int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
-                         int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st) {
+                         int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi,
+                         const void* d2, const void* yb, const uint8_t* mask, const float* mean,
+                         const float* scale, const float* shift) {
   if (!damd_conv_supported(C, K, cfg)) return -1;
+  if (epi < 0 || epi > 3 || (epi != 0 && part == nullptr)) return -3;
+  if (epi >= 2 && (yb == nullptr || mean == nullptr || (epi == 2 && mask == nullptr) ||
+                   (epi == 3 && (scale == nullptr || shift == nullptr))))
+    return -3;
   const Cfg c = kCfgs[cfg];
   Geo g;
   g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
@@ -519,23 +598,32 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   g.ptiles = static_cast<int>((g.M + c.bp - 1) / c.bp);
   g.ctiles = K / c.bco;
   g.groups = groups;
+  EpiArgs ea{static_cast<const bf16_t*>(d2), static_cast<const bf16_t*>(yb), mask, mean, scale, shift};
   const dim3 grid(static_cast<unsigned>(g.ctiles * groups));
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
-#define L(BCO, BP, WCO)                                                                                       \
-  do {                                                                                                        \
-    if (part) hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, true>), grid, dim3(kThreads), 0, st, xp, wp, yp, part, g); \
-    else hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, false>), grid, dim3(kThreads), 0, st, xp, wp, yp, part, g);     \
+#define L1(BCO, BP, WCO, NW, NST, E) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea)
+#define L(BCO, BP, WCO, NW, NST)                          \
+  do {                                                    \
+    switch (epi) {                                        \
+      case 0: L1(BCO, BP, WCO, NW, NST, kEpiNone); break;  \
+      case 1: L1(BCO, BP, WCO, NW, NST, kEpiStats); break; \
+      case 2: L1(BCO, BP, WCO, NW, NST, kEpiBnbM); break;  \
+      default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR); break; \
+    }                                                     \
   } while (0)
   switch (cfg) {
-    case 0: L(64, 128, 1); break;
-    case 1: L(128, 128, 2); break;
-    case 2: L(128, 256, 2); break;
-    case 3: L(64, 256, 1); break;
-    default: L(256, 128, 4); break;
+    case 0: L(64, 128, 1, 4, 2); break;
+    case 1: L(128, 128, 2, 4, 2); break;
+    case 2: L(64, 256, 1, 4, 2); break;
+    case 3: L(128, 256, 2, 8, 3); break;
+    case 4: L(64, 256, 1, 8, 3); break;
+    default: L(256, 128, 4, 8, 3); break;
   }
 #undef L
+#undef L1
   DAMD_CHECK_LAUNCH();
   return 0;
 }

@@ -14,7 +14,7 @@ from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 from determined_amd.ops import fusion_enabled
-from determined_amd.ops.conv import conv_bn_input, stem_conv2d
+from determined_amd.ops.conv import bn_act_conv, conv_bn_input, stem_conv2d
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -23,6 +23,12 @@ def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _chainable(blk: nn.Module) -> bool:
+    """Blocks whose forward is exactly the chained composition (no hooks on the block itself)."""
+    return (isinstance(blk, (Bottleneck, BasicBlock)) and not blk._forward_hooks
+            and not blk._forward_pre_hooks)
 
 
 def _downsample(ds: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -50,6 +56,12 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNormAct2d(cout)  # fused: relu(bn3(conv3) + identity)
         self.downsample = downsample
 
+    def convs(self):
+        return (self.conv1, self.conv2, self.conv3)
+
+    def bns(self):
+        return (self.bn1, self.bn2, self.bn3)
+
     def forward(self, x, split_grad: bool = False):
         """``x`` is a tensor or the ``(main, shortcut)`` pair of a split-gradient producer;
         ``split_grad`` makes this block's output such a pair (ops/bn.py).  Every conv hands its
@@ -64,6 +76,29 @@ class Bottleneck(nn.Module):
         return self.bn3(y, identity, split_grad=split_grad, stats_part=part)
 
 
+def _chain_blocks(blocks, x, split: bool):
+    """Run residual blocks back to back with every BN(+residual)+ReLU fused into the autograd node
+    of the conv that consumes it (ops/conv.py bn_act_conv), including a block's output BN with the
+    next block's first conv: the backward then fuses each BN's reduce pass into that conv's
+    input-gradient epilogue.  Returns the last block's output.  Blocks expose ``convs``/``bns``
+    (the main path, last BN takes the residual) and ``downsample``."""
+    pending = None  # (pre-BN output, its stats partials, residual, BN) of the previous block
+    for i, blk in enumerate(blocks):
+        convs, bns = blk.convs(), blk.bns()
+        if pending is None:
+            xm, xs = x if isinstance(x, tuple) else (x, x)
+            y, part = conv_bn_input(convs[0], xm)
+        else:
+            y_prev, p_prev, res_prev, bn_prev = pending
+            xs, y, part = bn_act_conv(bn_prev, y_prev, p_prev, res_prev, convs[0])
+        identity = xs if blk.downsample is None else _downsample(blk.downsample, xs)
+        for bn, conv in zip(bns[:-1], convs[1:]):
+            _, y, part = bn_act_conv(bn, y, part, None, conv)
+        pending = (y, part, identity, bns[-1])
+    y, part, identity, bn = pending
+    return bn(y, identity, stats_part=part)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -74,6 +109,12 @@ class BasicBlock(nn.Module):
         self.conv2 = conv3x3(width, width)
         self.bn2 = BatchNormAct2d(width)
         self.downsample = downsample
+
+    def convs(self):
+        return (self.conv1, self.conv2)
+
+    def bns(self):
+        return (self.bn1, self.bn2)
 
     def forward(self, x, split_grad: bool = False):
         xm, xs = x if isinstance(x, tuple) else (x, x)
@@ -133,8 +174,11 @@ class ResNet(nn.Module):
         y, part = stem_conv2d(self.conv1, x, with_stats=True)
         x = self.bn1.forward_maxpool(y, self.maxpool, split_grad=split, stats_part=part)
         blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
-        for i, blk in enumerate(blocks):
-            x = blk(x, split_grad=split and i + 1 < len(blocks))
+        if fusion_enabled("bn_conv") and all(_chainable(b) for b in blocks):
+            x = _chain_blocks(blocks, x, split)
+        else:
+            for i, blk in enumerate(blocks):
+                x = blk(x, split_grad=split and i + 1 < len(blocks))
         x = global_avg_pool(x)  # == flatten(self.avgpool(x), 1); fused channels-last backward
         return self.fc(x)
 

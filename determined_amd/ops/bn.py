@@ -45,6 +45,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, None if masked else residual, stats, weight, mask if masked else None)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.set_materialize_grads(False)  # _sum_grads takes a missing half of a split pair as None
         if split:
             return y, y.detach()
         return y
@@ -79,6 +80,7 @@ class _BNReLUPoolFn(torch.autograd.Function):
                                                     float(eps), stats_part)
         ctx.save_for_backward(x, idx, stats, weight, xarg)
         ctx.mark_non_differentiable(idx, xarg)
+        ctx.set_materialize_grads(False)
         if split:
             return y, y.detach()
         return y
@@ -171,6 +173,26 @@ class BatchNormAct2d(nn.BatchNorm2d):
         (``ops.conv.conv_bn_input``); training mode then skips the statistics pass."""
         y = self._forward(x, residual, split_grad, stats_part)
         return y if not split_grad or isinstance(y, tuple) else (y, y)
+
+    def train_step_args(self):
+        """(running_mean, running_var, momentum) for one training-mode forward; advances the host
+        batch counter (shared by the fused entry points, ops/conv.py bn_act_conv)."""
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self._nbt_host = self._nbt() + 1
+            if self.momentum is None:
+                momentum = 1.0 / float(self._nbt_host)
+        rm = self.running_mean if self.track_running_stats else None
+        rv = self.running_var if self.track_running_stats else None
+        return rm, rv, momentum
+
+    def kernel_path(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
+        """True when a training-mode forward of ``x`` runs on the fused HIP kernels."""
+        if not (self.training and x.is_cuda and self.affine):
+            return False
+        from determined_amd import ops
+
+        return bool(ops.ext().bn_supported(x)) and (residual is None or residual.stride() == x.stride())
 
     def _forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], split: bool,
                  stats_part: Optional[torch.Tensor] = None):

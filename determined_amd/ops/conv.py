@@ -31,6 +31,7 @@ class _StemConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         y, part = ops.ext().stem_conv_fwd(x, weight, bool(want_stats))
         ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
@@ -190,6 +191,7 @@ class _IGemmConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.geo = (stride, pad)
         ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         return y, part
 
     @staticmethod
@@ -241,3 +243,89 @@ def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple
 def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """``conv(x)`` on the implicit-GEMM kernels where supported (no statistics epilogue)."""
     return conv_bn_input(conv, x, stats=False)[0]
+
+
+# ------------------------------------------------------------------- BN(+residual)+ReLU -> conv
+class _BNActConvFn(torch.autograd.Function):
+    """``a = relu(bn(y) [+ residual])``, ``z = conv(a)`` (+ the BN statistic partials of z) as one
+    autograd node, so the backward can fuse the BN's reduce pass into the conv's input-gradient
+    epilogue (conv_igemm.hip kEpiBnb*): the gradient at the BN output -- the conv's dX plus the
+    gradient ``a`` received from its other consumer (a ResNet shortcut), ReLU-masked -- is
+    written once together with its (sum, sum * (y - mean)) partials, and the BN backward is left
+    with its finalize and a single apply pass.  Without the fused kernel (strided conv, config
+    unsupported) the backward is the unfused composition."""
+
+    @staticmethod
+    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg):
+        from determined_amd import ops
+
+        e = ops.ext()
+        a, stats, mask = e.bn_act_fwd(y, bn_w, bn_b, rm, rv, float(momentum), float(eps), residual, True, True,
+                                      stats_part)
+        z, part = e.conv_fwd(a, conv_w, stride, pad, True, cfg, 0)
+        masked = mask.numel() > 0
+        ctx.save_for_backward(y, stats, bn_w, mask if masked else None, a, conv_w,
+                              residual if (residual is not None and not masked) else None)
+        ctx.geo = (stride, pad, residual is not None)
+        ctx.mark_non_differentiable(part)
+        # an unused `a` (BN1/BN2 outputs have no second consumer) must arrive as None, not as a
+        # materialised zero tensor that the backward would read and add
+        ctx.set_materialize_grads(False)
+        return a, z, part
+
+    @staticmethod
+    def backward(ctx, g_a, g_z, _gpart=None):
+        from determined_amd import ops
+
+        e = ops.ext()
+        y, stats, bn_w, mask, a, conv_w, residual = ctx.saved_tensors
+        stride, pad, has_res = ctx.geo
+        cl = torch.channels_last
+        k = conv_w.shape[2]
+        if g_z is None:  # the conv output is always consumed in the networks this node serves
+            raise RuntimeError("bn_act_conv: the conv output received no gradient")
+        g_z = g_z.contiguous(memory_format=cl)
+        g_a = None if g_a is None else g_a.contiguous(memory_format=cl)
+        dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
+        wt = _flip_weight(conv_w) if stride == 1 and 2 * pad == k - 1 else None
+        fused = wt is not None and (mask is not None or not has_res) and bool(e.conv_supported(g_z, wt, -1))
+        if fused:
+            cands = {c: (lambda c=c: e.conv_dgrad_bn(g_z, wt, k - 1 - pad, c, g_a, y, mask, stats))
+                     for c in _igemm_cfgs(e, g_z, wt)}
+            key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+            dz, part = cands[_pick(key, cands, default=e.conv_default_cfg(wt.shape[0]))]()
+            dy, dg, db = e.bn_bwd_from_part(dz, y, stats, bn_w, part)
+            dres = dz if has_res else None
+        else:
+            da = _dgrad(g_z, a, conv_w, stride, pad).contiguous(memory_format=cl)
+            if g_a is not None and mask is None:
+                da, g_a = da + g_a, None
+            dy, dg, db, dres = e.bn_act_bwd(da, y, residual, stats, bn_w, True, has_res, mask, g_a)
+        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None)
+
+
+def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tensor], residual: Optional[torch.Tensor],
+                conv: nn.Conv2d) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+    """``a = bn(y, residual, stats_part=stats_part)`` (a ``BatchNormAct2d`` with ReLU) followed by
+    ``z, part = conv_bn_input(conv, a)``; returns ``(a, z, part)``.  Training-mode bf16
+    channels-last inputs run as one fused autograd node (:class:`_BNActConvFn`); anything else
+    is that exact composition."""
+    from determined_amd import ops
+    from determined_amd.ops.bn import BatchNormAct2d
+
+    if (isinstance(bn, BatchNormAct2d) and bn.act and _plain_module(bn) and ops.fusion_enabled("bn_conv")
+            and igemm_fusable(conv, y) and bn.kernel_path(y, residual) and y.shape[1] == conv.in_channels):
+        e = ops.ext()
+        rm, rv, momentum = bn.train_step_args()
+        st, pad = conv.stride[0], conv.padding[0]
+        w = conv.weight
+        key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
+        cfg = _TUNE.get(key)
+        if cfg is None:  # tune the conv on a stand-in input of the same shape
+            cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w)}
+            cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
+        return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,
+                                  cfg)
+    a = bn(y, residual, stats_part=stats_part)
+    z, part = conv_bn_input(conv, a)
+    return a, z, part

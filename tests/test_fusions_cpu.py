@@ -111,3 +111,23 @@ def test_resnet_forward_with_stats_path_matches_plain_on_cpu():
     x = torch.randn(2, 3, 32, 32)
     out = m(x)
     assert out.shape == (2, 10) and torch.isfinite(out).all()
+
+
+def test_chained_resnet_forward_equals_per_block_on_cpu(monkeypatch):
+    """The fused block chain (models/resnet.py _chain_blocks) is the exact per-block composition
+    on CPU (its fused autograd nodes only engage on the GPU)."""
+    import determined_amd.ops as ops
+    from determined_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).train()
+    x = torch.randn(2, 3, 64, 64)
+    outs = []
+    for disabled in (frozenset(), frozenset({"bn_conv"})):
+        monkeypatch.setattr(ops, "_DISABLED", disabled)
+        m.zero_grad()
+        out = m(x)
+        out.square().sum().backward()
+        outs.append((out.detach(), m.layer2[1].conv2.weight.grad.clone()))
+    torch.testing.assert_close(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1], outs[1][1])

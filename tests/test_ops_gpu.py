@@ -408,3 +408,74 @@ def test_bottleneck_grads_with_and_without_conv_kernels(ops, monkeypatch, cin, w
         assert e_on < max(2 * e_off, 3e-2), (n, e_on, e_off)
 
 
+
+
+@pytest.mark.parametrize("k,masked,with_d2", [(1, True, True), (1, True, False), (3, False, False), (1, False, False)])
+def test_conv_dgrad_bn_epilogue(ops, k, masked, with_d2):
+    """conv_dgrad_bn: dz = (dX [+ d2]) * relu-mask and the BN-backward partials, vs torch."""
+    e = ops.ext()
+    torch.manual_seed(0)
+    n, cin, cout, hw = 4, 128, 64, 10
+    cl = torch.channels_last
+    w = (torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    g = torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yb = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    bnw = torch.rand(cin, device="cuda") + 0.5
+    bnb = torch.randn(cin, device="cuda") * 0.2
+    res = torch.randn_like(yb) if masked else None
+    a, stats, mask = e.bn_act_fwd(yb, bnw, bnb, None, None, 0.0, 1e-5, res, True, True, None)
+    assert (mask.numel() > 0) == masked
+    d2 = torch.randn_like(yb) if with_d2 else None
+    wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)
+    dz, part = e.conv_dgrad_bn(g, wt, k // 2, -1, d2, yb, mask if masked else None, stats)
+    da = torch.nn.grad.conv2d_input(yb.shape, w.float(), g.float(), padding=k // 2)
+    if with_d2:
+        da = da + d2.float()
+    ref = da * (a.float() > 0)
+    torch.testing.assert_close(dz.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    dzf = dz.float()
+    torch.testing.assert_close(part[:, 0].sum(0), dzf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    cen = yb.float() - stats[0].view(1, -1, 1, 1)
+    torch.testing.assert_close(part[:, 1].sum(0), (dzf * cen).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("depth", [3])
+def test_chained_bottlenecks_match_unchained(ops, monkeypatch, depth):
+    """ResNet block chain with every BN fused into its consumer conv's autograd node (ops/conv.py
+    bn_act_conv) vs per-block forwards, both against an fp32 reference."""
+    import copy
+    from determined_amd.models.resnet import Bottleneck, _chain_blocks
+    from determined_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(0)
+    ds = torch.nn.Sequential(torch.nn.Conv2d(64, 256, 1, bias=False), BatchNormAct2d(256, act=False))
+    blocks = torch.nn.ModuleList([Bottleneck(64, 64, 1, ds)] + [Bottleneck(256, 64) for _ in range(depth - 1)])
+    for mod in blocks.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    x0 = torch.randn(8, 64, 16, 16)
+    g0 = torch.randn(8, 256, 16, 16)
+
+    def run(dtype, chained):
+        monkeypatch.setattr(ops, "_DISABLED", frozenset() if chained else frozenset({"bn_conv"}))
+        bl = copy.deepcopy(blocks).cuda().to(dtype).to(memory_format=torch.channels_last)
+        x = x0.cuda().to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        if chained:
+            y = _chain_blocks(list(bl), x, False)
+        else:
+            y = x
+            for b in bl:
+                y = b(y)
+        y.backward(g0.cuda().to(dtype).contiguous(memory_format=torch.channels_last))
+        grads = {n: p.grad.float().cpu() for n, p in bl.named_parameters()}
+        grads["x"] = x.grad.float().cpu()
+        return y.detach().float().cpu(), grads
+
+    yr, ref = run(torch.float32, False)
+    yc, on = run(torch.bfloat16, True)
+    yu, off = run(torch.bfloat16, False)
+    assert ((yc - yr).norm() / yr.norm()).item() < 2e-2
+    for n, r in ref.items():
+        e_on = ((on[n] - r).norm() / r.norm()).item()
+        e_off = ((off[n] - r).norm() / r.norm()).item()
+        assert e_on < max(2 * e_off, 3e-2), (n, e_on, e_off)
