@@ -118,7 +118,12 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   constexpr int NIW = BCO / (8 * NW), NIX = BP / (8 * NW);  // DMA instructions per wave per stage
   constexpr int NL = NIW + NIX;
   static_assert(NL * (NST - 2) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE];
+  // one LDS array (a second __shared__ object makes hipcc wait for every DMA before each
+  // ds_read): NST ring slots, then the block's per-channel BN parameters for the BN-backward
+  // epilogues (mean, scale, shift of its BCO output channels; the co tile is fixed per block)
+  constexpr int PARAMS = EPI >= kEpiBnbM ? 3 * BCO * 2 : 0;  // in bf16_t units (3 x BCO floats)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE + PARAMS];
+  float* prm = reinterpret_cast<float*>(lds + NST * STAGE);
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rho = lane & 15, lg = lane >> 4;
@@ -132,6 +137,14 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   const int ntiles = grp < g.ptiles ? (g.ptiles - grp + g.groups - 1) / g.groups : 0;
   const int items = ntiles * g.ksteps;
   const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
+  if (EPI >= kEpiBnbM) {  // visible to every wave after the main loop's first barrier
+    for (int t = threadIdx.x; t < BCO; t += NT) {
+      const int co = ct * BCO + t;
+      prm[t] = ea.mean[co];
+      prm[BCO + t] = EPI == kEpiBnbR ? ea.scale[co] : 0.f;
+      prm[2 * BCO + t] = EPI == kEpiBnbR ? ea.shift[co] : 0.f;
+    }
+  }
 
   // ---- DMA lane roles: lane -> (row within its 8-row piece, 16-byte slot)
   const int prow = lane >> 3, slot = lane & 7;
@@ -241,67 +254,90 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
     }
     if (++c_ks == g.ksteps) {
-      // epilogue: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel wp0 + 16j + rho
+      // epilogue: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel wp0 + 16j + rho.
+      // Done in halves over j: the BN-backward operand loads of a half are all issued first
+      // (unconditionally, tail rows clamped to row 0, a missing d2 replaced by yb and scaled
+      // by 0) so they overlap instead of each load waiting before the next is issued.
       const int64_t pt = grp + static_cast<int64_t>(c_tile) * g.groups;
+      constexpr int JH = FJ >= 2 ? FJ / 2 : 1;
+      const bf16_t* d2p = ea.d2 != nullptr ? ea.d2 : ea.yb;
+      const float d2f = ea.d2 != nullptr ? 1.f : 0.f;
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        const int64_t m = pt * BP + wp0 + 16 * j + rho;
-        const bool ok = m < g.M;
+      for (int j0 = 0; j0 < FJ; j0 += JH) {
+        bf16x8 dv[JH][FI / 2], yr[JH][FI / 2];
+        uint32_t mb[JH][FI / 2];
+        if (EPI >= kEpiBnbM) {
 #pragma unroll
-        for (int q = 0; q < FI / 2; ++q) {
-          const int64_t co = static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
-          float o[8];
+          for (int jj = 0; jj < JH; ++jj) {
+            const int64_t m = pt * BP + wp0 + 16 * (j0 + jj) + rho;
+            const int64_t ms = m < g.M ? m : 0;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
-          float yv[8];
-          if (EPI >= kEpiBnbM && ok) {
-            if (ea.d2 != nullptr) {
-              const bf16x8 dv = *reinterpret_cast<const bf16x8*>(ea.d2 + m * g.K + co);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o[e] += bf2f(dv.v[e]);
-            }
-            const bf16x8 yr = *reinterpret_cast<const bf16x8*>(ea.yb + m * g.K + co);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) yv[e] = bf2f(yr.v[e]);
-            if (EPI == kEpiBnbM) {
-              const uint32_t mb = ea.mask[(m * g.K + co) >> 3];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o[e] = (mb >> e) & 1u ? o[e] : 0.f;
-            } else {
-              const float4 s0 = *reinterpret_cast<const float4*>(ea.scale + co);
-              const float4 s1 = *reinterpret_cast<const float4*>(ea.scale + co + 4);
-              const float4 h0 = *reinterpret_cast<const float4*>(ea.shift + co);
-              const float4 h1 = *reinterpret_cast<const float4*>(ea.shift + co + 4);
-              const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-              const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o[e] = yv[e] * sc[e] + sh[e] > 0.f ? o[e] : 0.f;
+            for (int q = 0; q < FI / 2; ++q) {
+              const int64_t off = ms * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+              yr[jj][q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
+              dv[jj][q] = *reinterpret_cast<const bf16x8*>(d2p + off);
+              if (EPI == kEpiBnbM) mb[jj][q] = ea.mask[off >> 3];
             }
           }
-          bf16x8 v;
+        }
 #pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            const u16v2_t pk = f2bf2(o[e], o[e + 1]);
-            v.v[e] = pk[0]; v.v[e + 1] = pk[1];
-          }
-          if (ok) {
-            *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
-            if (EPI == kEpiStats) {
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          const int64_t m = pt * BP + wp0 + 16 * j + rho;
+          const bool ok = m < g.M;
+#pragma unroll
+          for (int q = 0; q < FI / 2; ++q) {
+            const int cl = wco0 + 32 * q + 8 * lg;  // channel within the block's co tile
+            const int64_t co = static_cast<int64_t>(ct) * BCO + cl;
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
+            float yv[8];
+            if (EPI >= kEpiBnbM) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
-                const float f = bf2f(v.v[e]);
-                st_s[q][e] += f;
-                st_q[q][e] += f * f;
+                yv[e] = bf2f(yr[jj][q].v[e]);
+                o[e] += d2f * bf2f(dv[jj][q].v[e]);
               }
-            } else if (EPI >= kEpiBnbM) {
-              const float4 u0 = *reinterpret_cast<const float4*>(ea.mean + co);
-              const float4 u1 = *reinterpret_cast<const float4*>(ea.mean + co + 4);
-              const float mu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+              if (EPI == kEpiBnbM) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const float f = bf2f(v.v[e]);  // the stored (rounded) dz, as the apply pass reads it
-                st_s[q][e] += f;
-                st_q[q][e] += f * (yv[e] - mu[e]);
+                for (int e = 0; e < 8; ++e) o[e] = (mb[jj][q] >> e) & 1u ? o[e] : 0.f;
+              } else {
+                const float4 s0 = *reinterpret_cast<const float4*>(prm + BCO + cl);
+                const float4 s1 = *reinterpret_cast<const float4*>(prm + BCO + cl + 4);
+                const float4 h0 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl);
+                const float4 h1 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl + 4);
+                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = yv[e] * sc[e] + sh[e] > 0.f ? o[e] : 0.f;
+              }
+            }
+            bf16x8 v;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const u16v2_t pk = f2bf2(o[e], o[e + 1]);
+              v.v[e] = pk[0]; v.v[e + 1] = pk[1];
+            }
+            if (ok) {
+              *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
+              if (EPI == kEpiStats) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  const float f = bf2f(v.v[e]);
+                  st_s[q][e] += f;
+                  st_q[q][e] += f * f;
+                }
+              } else if (EPI >= kEpiBnbM) {
+                const float4 u0 = *reinterpret_cast<const float4*>(prm + cl);
+                const float4 u1 = *reinterpret_cast<const float4*>(prm + cl + 4);
+                const float mu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  const float f = bf2f(v.v[e]);  // the stored (rounded) dz, as the apply pass reads it
+                  st_s[q][e] += f;
+                  st_q[q][e] += f * (yv[e] - mu[e]);
+                }
               }
             }
           }
