@@ -59,8 +59,8 @@ void damd_col_reduce_launch(const float*, float*, int, int, hipStream_t);
 // launchers (conv_igemm.hip)
 extern "C" int damd_conv_num_cfgs();
 extern "C" int damd_conv_default_cfg(int, int64_t);
-extern "C" int damd_conv_supported(int, int, int);
-extern "C" int damd_conv_groups(int64_t, int, int, int);
+extern "C" int damd_conv_supported(int, int, int, int, int, int, int, int);
+extern "C" int damd_conv_groups(int64_t, int, int, int, int);
 extern "C" int damd_wgrad_num_cfgs();
 extern "C" int damd_wgrad_supported(int, int, int);
 extern "C" int damd_wgrad_splits(int64_t, int, int, int, int, int, int);
@@ -666,18 +666,20 @@ at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::
 // ---------------------------------------------------------------- implicit-GEMM convolution
 // x: [N, C, H, W] bf16 channels-last; w: [K, C, R, S] bf16 (made channels-last = [K][R][S][C]);
 // returns (y [N, K, OH, OW] channels-last, stats partials [groups, 2, K] or an empty tensor).
-bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg) {
+bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg, int64_t stride, int64_t pad) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
   return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
          w.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.size(1) == x.size(1) &&
-         damd_conv_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(cfg));
+         damd_conv_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(w.size(2)),
+                             static_cast<int>(w.size(3)), static_cast<int>(stride), static_cast<int>(pad),
+                             static_cast<int>(x.size(3)), static_cast<int>(cfg));
 }
 
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  bool want_stats, int64_t cfg, int64_t groups) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
-  TORCH_CHECK(conv_supported(x, w, cfg), "conv_fwd: unsupported input / weight / config");
+  TORCH_CHECK(conv_supported(x, w, cfg, stride, pad), "conv_fwd: unsupported input / weight / config");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t K = w.size(0), R = w.size(2), S = w.size(3);
   TORCH_CHECK(stride >= 1 && pad >= 0 && H + 2 * pad >= R && W + 2 * pad >= S, "conv_fwd: bad geometry");
@@ -686,7 +688,8 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   TORCH_CHECK(M < (int64_t{1} << 31) - 4096 && x.numel() < (int64_t{1} << 40), "conv_fwd: tensor too large");
   auto wl = w.contiguous(at::MemoryFormat::ChannelsLast);
   auto y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(cfg), static_cast<int>(groups));
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg),
+                                 static_cast<int>(groups));
   at::Tensor part = want_stats ? at::empty({G, 2, K}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
   const int rc = damd_conv_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
@@ -707,7 +710,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
                                       const c10::optional<at::Tensor>& d2, const at::Tensor& yb,
                                       const c10::optional<at::Tensor>& mask, const at::Tensor& stats) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(wt.size(0)), 0);
-  TORCH_CHECK(conv_supported(dy, wt, cfg), "conv_dgrad_bn: unsupported input / weight / config");
+  TORCH_CHECK(conv_supported(dy, wt, cfg, 1, pad), "conv_dgrad_bn: unsupported input / weight / config");
   const int64_t N = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
   const int64_t K = wt.size(0), R = wt.size(2), S = wt.size(3);
   TORCH_CHECK(R == S && 2 * pad == R - 1, "conv_dgrad_bn: stride-1 same-size convolutions only");
@@ -732,7 +735,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
   TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_dgrad_bn: tensor too large");
   auto wl = wt.contiguous(at::MemoryFormat::ChannelsLast);
   auto dz = at::empty_like(yb);
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(cfg), 0);
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
   auto part = at::empty({G, 2, K}, dy.options().dtype(at::kFloat));
   const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),

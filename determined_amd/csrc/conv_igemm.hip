@@ -103,6 +103,144 @@ struct EpiArgs {
   const float* shift;
 };
 
+// Tile epilogue shared by the conv kernels (EPI modes above): stores the BP x BCO output tile of
+// pixel tile pt / co tile ct from the accumulators, accumulating the per-lane channel sums.
+template <int BCO, int BP, int FI, int FJ, int EPI>
+__device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t pt, int ct, int wco0, int wp0, int lg,
+                                               int rho, const Geo& g, const EpiArgs& ea, const float* prm,
+                                               bf16_t* __restrict__ y, float (&st_s)[FI / 2][8],
+                                               float (&st_q)[FI / 2][8]) {
+  // epilogue: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel wp0 + 16j + rho.
+  // Done in halves over j: the BN-backward operand loads of a half are all issued first
+  // (unconditionally, tail rows clamped to row 0, a missing d2 replaced by yb and scaled
+  // by 0) so they overlap instead of each load waiting before the next is issued.
+  constexpr int JH = FJ >= 2 ? FJ / 2 : 1;
+  const bf16_t* d2p = ea.d2 != nullptr ? ea.d2 : ea.yb;
+  const float d2f = ea.d2 != nullptr ? 1.f : 0.f;
+#pragma unroll
+  for (int j0 = 0; j0 < FJ; j0 += JH) {
+    bf16x8 dv[JH][FI / 2], yr[JH][FI / 2];
+    uint32_t mb[JH][FI / 2];
+    if (EPI >= kEpiBnbM) {
+#pragma unroll
+      for (int jj = 0; jj < JH; ++jj) {
+        const int64_t m = pt * BP + wp0 + 16 * (j0 + jj) + rho;
+        const int64_t ms = m < g.M ? m : 0;
+#pragma unroll
+        for (int q = 0; q < FI / 2; ++q) {
+          const int64_t off = ms * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+          yr[jj][q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
+          dv[jj][q] = *reinterpret_cast<const bf16x8*>(d2p + off);
+          if (EPI == kEpiBnbM) mb[jj][q] = ea.mask[off >> 3];
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < JH; ++jj) {
+      const int j = j0 + jj;
+      const int64_t m = pt * BP + wp0 + 16 * j + rho;
+      const bool ok = m < g.M;
+#pragma unroll
+      for (int q = 0; q < FI / 2; ++q) {
+        const int cl = wco0 + 32 * q + 8 * lg;  // channel within the block's co tile
+        const int64_t co = static_cast<int64_t>(ct) * BCO + cl;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
+        float yv[8];
+        if (EPI >= kEpiBnbM) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            yv[e] = bf2f(yr[jj][q].v[e]);
+            o[e] += d2f * bf2f(dv[jj][q].v[e]);
+          }
+          if (EPI == kEpiBnbM) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (mb[jj][q] >> e) & 1u ? o[e] : 0.f;
+          } else {
+            const float4 s0 = *reinterpret_cast<const float4*>(prm + BCO + cl);
+            const float4 s1 = *reinterpret_cast<const float4*>(prm + BCO + cl + 4);
+            const float4 h0 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl);
+            const float4 h1 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl + 4);
+            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = yv[e] * sc[e] + sh[e] > 0.f ? o[e] : 0.f;
+          }
+        }
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const u16v2_t pk = f2bf2(o[e], o[e + 1]);
+          v.v[e] = pk[0]; v.v[e + 1] = pk[1];
+        }
+        if (ok) {
+          *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
+          if (EPI == kEpiStats) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float f = bf2f(v.v[e]);
+              st_s[q][e] += f;
+              st_q[q][e] += f * f;
+            }
+          } else if (EPI >= kEpiBnbM) {
+            const float4 u0 = *reinterpret_cast<const float4*>(prm + cl);
+            const float4 u1 = *reinterpret_cast<const float4*>(prm + cl + 4);
+            const float mu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float f = bf2f(v.v[e]);  // the stored (rounded) dz, as the apply pass reads it
+              st_s[q][e] += f;
+              st_q[q][e] += f * (yv[e] - mu[e]);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// Block-level reduction of the epilogue channel sums into part[grp][2][K] (LDS reused: call
+// after the last fragment read).
+template <int BCO, int FI, int WCO, int NW>
+__device__ __forceinline__ void epi_flush_sums(float (&st_s)[FI / 2][8], float (&st_q)[FI / 2][8], bf16_t* lds,
+                                               int wave, int lg, int rho, int wco0, int grp, int ct, int K,
+                                               float* __restrict__ part) {
+  constexpr int NT = 64 * NW, WP = NW / WCO;
+  // sum over the 16 pixel lanes of each lane group, then over the WP waves sharing a co range
+#pragma unroll
+  for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        st_s[q][e] += __shfl_xor(st_s[q][e], o, 64);
+        st_q[q][e] += __shfl_xor(st_q[q][e], o, 64);
+      }
+  __syncthreads();  // LDS reuse: every wave is past its last fragment read
+  float* red = reinterpret_cast<float*>(lds);  // [WP][2][BCO]
+  const int wpi = wave / WCO;
+  if (rho == 0) {
+#pragma unroll
+    for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = wco0 + 32 * q + 8 * lg + e;
+        red[(wpi * 2) * BCO + co] = st_s[q][e];
+        red[(wpi * 2 + 1) * BCO + co] = st_q[q][e];
+      }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * BCO; t += NT) {
+    const int which = t / BCO, co = t - which * BCO;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < WP; ++k) s += red[(k * 2 + which) * BCO + co];
+    part[(static_cast<int64_t>(grp) * 2 + which) * K + static_cast<int64_t>(ct) * BCO + co] = s;
+  }
+}
+
+
 template <int BCO, int BP, int WCO, int NW, int NST, int EPI>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
@@ -254,95 +392,8 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
     }
     if (++c_ks == g.ksteps) {
-      // epilogue: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel wp0 + 16j + rho.
-      // Done in halves over j: the BN-backward operand loads of a half are all issued first
-      // (unconditionally, tail rows clamped to row 0, a missing d2 replaced by yb and scaled
-      // by 0) so they overlap instead of each load waiting before the next is issued.
-      const int64_t pt = grp + static_cast<int64_t>(c_tile) * g.groups;
-      constexpr int JH = FJ >= 2 ? FJ / 2 : 1;
-      const bf16_t* d2p = ea.d2 != nullptr ? ea.d2 : ea.yb;
-      const float d2f = ea.d2 != nullptr ? 1.f : 0.f;
-#pragma unroll
-      for (int j0 = 0; j0 < FJ; j0 += JH) {
-        bf16x8 dv[JH][FI / 2], yr[JH][FI / 2];
-        uint32_t mb[JH][FI / 2];
-        if (EPI >= kEpiBnbM) {
-#pragma unroll
-          for (int jj = 0; jj < JH; ++jj) {
-            const int64_t m = pt * BP + wp0 + 16 * (j0 + jj) + rho;
-            const int64_t ms = m < g.M ? m : 0;
-#pragma unroll
-            for (int q = 0; q < FI / 2; ++q) {
-              const int64_t off = ms * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
-              yr[jj][q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
-              dv[jj][q] = *reinterpret_cast<const bf16x8*>(d2p + off);
-              if (EPI == kEpiBnbM) mb[jj][q] = ea.mask[off >> 3];
-            }
-          }
-        }
-#pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int j = j0 + jj;
-          const int64_t m = pt * BP + wp0 + 16 * j + rho;
-          const bool ok = m < g.M;
-#pragma unroll
-          for (int q = 0; q < FI / 2; ++q) {
-            const int cl = wco0 + 32 * q + 8 * lg;  // channel within the block's co tile
-            const int64_t co = static_cast<int64_t>(ct) * BCO + cl;
-            float o[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
-            float yv[8];
-            if (EPI >= kEpiBnbM) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                yv[e] = bf2f(yr[jj][q].v[e]);
-                o[e] += d2f * bf2f(dv[jj][q].v[e]);
-              }
-              if (EPI == kEpiBnbM) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = (mb[jj][q] >> e) & 1u ? o[e] : 0.f;
-              } else {
-                const float4 s0 = *reinterpret_cast<const float4*>(prm + BCO + cl);
-                const float4 s1 = *reinterpret_cast<const float4*>(prm + BCO + cl + 4);
-                const float4 h0 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl);
-                const float4 h1 = *reinterpret_cast<const float4*>(prm + 2 * BCO + cl + 4);
-                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = yv[e] * sc[e] + sh[e] > 0.f ? o[e] : 0.f;
-              }
-            }
-            bf16x8 v;
-#pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-              const u16v2_t pk = f2bf2(o[e], o[e + 1]);
-              v.v[e] = pk[0]; v.v[e + 1] = pk[1];
-            }
-            if (ok) {
-              *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
-              if (EPI == kEpiStats) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const float f = bf2f(v.v[e]);
-                  st_s[q][e] += f;
-                  st_q[q][e] += f * f;
-                }
-              } else if (EPI >= kEpiBnbM) {
-                const float4 u0 = *reinterpret_cast<const float4*>(prm + cl);
-                const float4 u1 = *reinterpret_cast<const float4*>(prm + cl + 4);
-                const float mu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const float f = bf2f(v.v[e]);  // the stored (rounded) dz, as the apply pass reads it
-                  st_s[q][e] += f;
-                  st_q[q][e] += f * (yv[e] - mu[e]);
-                }
-              }
-            }
-          }
-        }
-      }
+      epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, grp + static_cast<int64_t>(c_tile) * g.groups, ct, wco0, wp0, lg, rho,
+                                           g, ea, prm, y, st_s, st_q);
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -352,41 +403,177 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
   }
 
+  if (SUMS) epi_flush_sums<BCO, FI, WCO, NW>(st_s, st_q, lds, wave, lg, rho, wco0, grp, ct, g.K, part);
+}
+
+
+
+// =============================================================================== 3x3 halo kernel
+// 3x3 / stride 1 / pad 1 convolution (forward, or the input gradient with flipped weights).  The
+// generic kernel re-gathers the im2col rows of every tap (9 x BP pixel rows per 64 channels) and
+// is bound by the LDS-DMA gather rate from L2 (~52 GB/s per CU measured: 256-ch 3x3 at 14x14 in
+// profiles/conv_igemm_*).  Here the pixel tile's input halo -- the BP + 2W + 2 consecutive input
+// pixels m0 - W - 1 ... (stride 1 keeps the flattened input and output pixel index aligned) -- is
+// staged ONCE per 64-channel block and all 9 taps read it at row offset r*W + s; a per-pixel
+// 9-bit tap-validity mask zeroes the fragments whose tap falls outside the image (the flattened
+// neighbour belongs to another row or image).  Weights stream per tap through a 3-slot ring.
+// Halo image swizzle: chunk c of row k at slot c ^ (k & 7) -- conflict-free for 16 consecutive
+// rows starting at ANY row (the taps shift the fragment rows by r*W + s).
+constexpr int kHaloMaxLds = 160 * 1024;
+
+template <int BCO, int BP, int WCO, int NW, int EPI>
+__global__ void __launch_bounds__(64 * NW, 2)
+conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+               float* __restrict__ part, Geo g, EpiArgs ea, int HR) {
+  constexpr bool SUMS = EPI != kEpiNone;
+  constexpr int NT = 64 * NW;
+  constexpr int WP = NW / WCO;
+  constexpr int TCO = BCO / WCO, TP = BP / WP;
+  constexpr int FI = TCO / 16, FJ = TP / 16;
+  static_assert(WCO * WP == NW && FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0, "bad tile");
+  constexpr int NIW = BCO / (8 * NW);
+  constexpr int WSLOT = BCO * kBK;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int HSLOT = HR * kBK;
+  bf16_t* halo = lds;               // [2][HR][64]
+  bf16_t* wts = lds + 2 * HSLOT;    // [3][BCO][64]
+  float* prm = reinterpret_cast<float*>(wts + 3 * WSLOT);
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rho = lane & 15, lg = lane >> 4;
+  const int wco0 = (wave % WCO) * TCO, wp0 = (wave / WCO) * TP;
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ct = rid % g.ctiles, grp = rid / g.ctiles;
+  const int ntiles = grp < g.ptiles ? (g.ptiles - grp + g.groups - 1) / g.groups : 0;
+  const int items = ntiles * g.ksteps;  // ksteps = 9 * cblk, tap fastest
+  const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
+  if (EPI >= kEpiBnbM) {
+    for (int t = threadIdx.x; t < BCO; t += NT) {
+      const int co = ct * BCO + t;
+      prm[t] = ea.mean[co];
+      prm[BCO + t] = EPI == kEpiBnbR ? ea.scale[co] : 0.f;
+      prm[2 * BCO + t] = EPI == kEpiBnbR ? ea.shift[co] : 0.f;
+    }
+  }
+  const int prow = lane >> 3, slot = lane & 7;
+  const bf16_t* wsrc[NIW];
+#pragma unroll
+  for (int i = 0; i < NIW; ++i) {
+    const int co = 8 * (wave + NW * i) + prow;
+    wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
+  }
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+
+  // load side: (tile, channel block, tap) counters, running halo count (slot parity)
+  int l_tile = 0, l_cb = 0, l_tap = 0, l_halo = 0;
+  auto issue = [&](int wslot) {
+    if (l_tap == 0) {  // stage this tile's halo for channel block l_cb
+      const int64_t f0 = static_cast<int64_t>(grp + l_tile * g.groups) * BP - g.W - 1;
+      bf16_t* hs = halo + (l_halo & 1) * HSLOT;
+      for (int k0 = 8 * wave; k0 < HR; k0 += 8 * NW) {
+        const int k = k0 + prow;
+        const int64_t f = f0 + k;
+        const bf16_t* src = (f >= 0 && f < g.M) ? x + f * g.C + l_cb * kBK + ((slot ^ (k & 7)) << 3) : zero;
+        dma16(src, hs + k0 * kBK);
+      }
+      ++l_halo;
+    }
+    bf16_t* ws = wts + wslot * WSLOT;
+    const int koff = l_tap * g.C + l_cb * kBK;
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + koff, ws + 8 * (wave + NW * i) * kBK);
+    if (++l_tap == 9) {
+      l_tap = 0;
+      if (++l_cb == g.cblk) { l_cb = 0; ++l_tile; }
+    }
+  };
+
+  f4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float st_s[FI / 2][8], st_q[FI / 2][8];
   if (SUMS) {
-    // sum over the 16 pixel lanes of each lane group, then over the WP waves sharing a co range
 #pragma unroll
     for (int q = 0; q < FI / 2; ++q)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
+      for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
+  }
+  uint32_t vm[FJ];  // per fragment pixel: bit 3r+s = tap (r, s) inside the image
+
+  if (items > 0) issue(0);
+  if (items > 1) issue(1);
+  int c_tap = 0, c_cb = 0, c_tile = 0, c_halo = 0;
+  for (int it = 0; it < items; ++it) {
+    // the next item's DMAs may stay in flight (a halo issued with it is over-waited: correct)
+    if (it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + 2 < items) issue((it + 2) % 3);
+    const int64_t pt = grp + static_cast<int64_t>(c_tile) * g.groups;
+    if (c_tap == 0 && c_cb == 0) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          st_s[q][e] += __shfl_xor(st_s[q][e], o, 64);
-          st_q[q][e] += __shfl_xor(st_q[q][e], o, 64);
+      for (int j = 0; j < FJ; ++j) {
+        const int64_t m = pt * BP + wp0 + 16 * j + rho;
+        uint32_t bits = 0;
+        if (m < g.M) {
+          const int64_t hw = m / g.W;
+          const int ww = static_cast<int>(m - hw * g.W);
+          const int hh = static_cast<int>(hw % g.H);
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int s2 = 0; s2 < 3; ++s2) {
+              const bool ok = hh + r - 1 >= 0 && hh + r - 1 < g.H && ww + s2 - 1 >= 0 && ww + s2 - 1 < g.W;
+              bits |= (ok ? 1u : 0u) << (3 * r + s2);
+            }
         }
-    __syncthreads();  // LDS reuse: every wave is past its last fragment read
-    float* red = reinterpret_cast<float*>(lds);  // [WP][2][BCO]
-    const int wpi = wave / WCO;
-    if (rho == 0) {
-#pragma unroll
-      for (int q = 0; q < FI / 2; ++q)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int co = wco0 + 32 * q + 8 * lg + e;
-          red[(wpi * 2) * BCO + co] = st_s[q][e];
-          red[(wpi * 2 + 1) * BCO + co] = st_q[q][e];
-        }
+        vm[j] = bits;
+      }
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < 2 * BCO; t += NT) {
-      const int which = t / BCO, co = t - which * BCO;
-      float s = 0.f;
+    const bf16_t* sw = wts + (it % 3) * WSLOT;
+    const bf16_t* sh = halo + (c_halo & 1) * HSLOT;
+    const int rowoff = (c_tap / 3) * g.W + (c_tap % 3);
 #pragma unroll
-      for (int k = 0; k < WP; ++k) s += red[(k * 2 + which) * BCO + co];
-      part[(static_cast<int64_t>(grp) * 2 + which) * g.K + static_cast<int64_t>(ct) * BCO + co] = s;
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lg;
+      s8 a[FI], b[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int row = wco0 + a_row(i, rho);
+        a[i] = *reinterpret_cast<const s8*>(sw + row * kBK + ((chunk ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int row = wp0 + 16 * j + rho + rowoff;
+        const s8 v = *reinterpret_cast<const s8*>(sh + row * kBK + ((chunk ^ (row & 7)) << 3));
+        const bool ok = (vm[j] >> c_tap) & 1u;
+        b[j] = ok ? v : s8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+    if (++c_tap == 9) {
+      c_tap = 0;
+      ++c_halo;
+      if (++c_cb == g.cblk) {
+        c_cb = 0;
+        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        ++c_tile;
+      }
     }
   }
+  if (SUMS) epi_flush_sums<BCO, FI, WCO, NW>(st_s, st_q, lds, wave, lg, rho, wco0, grp, ct, g.K, part);
 }
-
 
 // =============================================================================== weight gradient
 // dW[co][k] = sum_p dY[p][co] . im2col[p][k], k = (r, s, c): rows co, columns k, reduction over
@@ -537,17 +724,32 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
       }
 }
 
-// dW = sum over splits (fixed order) of part[split][n], 4 consecutive outputs per thread.
+// dW = sum over splits of part[split][n], 4 consecutive outputs per thread; eight independent
+// partial sums (splits k, k+8, ...) keep eight loads in flight instead of one dependent chain,
+// combined in a fixed order (deterministic).
 template <typename WT>
 __global__ void __launch_bounds__(256)
 wgrad_finalize_kernel(const float* __restrict__ part, int splits, int64_t n, WT* __restrict__ dw) {
   const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
   if (i >= n) return;
-  float4 s = *reinterpret_cast<const float4*>(part + i);
-  for (int k = 1; k < splits; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + i);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  float4 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = 0;
+  for (; k + 8 <= splits; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k + u) * n + i);
+      a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+    }
   }
+  for (; k < splits; ++k) {  // tail (< 8 splits) into one accumulator: no runtime-indexed array
+    const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + i);
+    a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+  }
+  float4 s = a[0];
+#pragma unroll
+  for (int u = 1; u < 8; ++u) { s.x += a[u].x; s.y += a[u].y; s.z += a[u].z; s.w += a[u].w; }
   Elem<WT>::st(dw, i, s.x);
   Elem<WT>::st(dw, i + 1, s.y);
   Elem<WT>::st(dw, i + 2, s.z);
@@ -568,12 +770,21 @@ struct Cfg {
 };
 // 0-2: 4 waves, 2-slot ring; 3-5: 8 waves, 3-slot ring (the tiles that won on some ResNet-50
 // layer in profiles/conv_igemm_*; 128x256 / 256x128 with 4 waves spill and never won)
+// nst = 0 marks the 3x3 halo kernel (stride-1 3x3 only)
 constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2},  {128, 128, 2, 4, 2}, {64, 256, 1, 4, 2},
-                         {128, 256, 2, 8, 3}, {64, 256, 1, 8, 3},  {256, 128, 4, 8, 3}};
+                         {128, 256, 2, 8, 3}, {64, 256, 1, 8, 3},  {256, 128, 4, 8, 3},
+                         {128, 256, 2, 8, 0}, {64, 256, 1, 8, 0},  {128, 128, 2, 4, 0},
+                         {256, 128, 4, 8, 0}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-int blocks_per_cu(const Cfg& c) {
-  const int lds = c.nst * (c.bco + c.bp) * kBK * 2;
+int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
+
+int halo_lds_bytes(const Cfg& c, int W) {
+  return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4;
+}
+
+int blocks_per_cu(const Cfg& c, int W = 0) {
+  const int lds = c.nst == 0 ? halo_lds_bytes(c, W) : c.nst * (c.bco + c.bp) * kBK * 2;
   int occ = (160 * 1024) / lds;
   const int by_waves = 8 / c.nw;  // __launch_bounds__(64 * NW, 2): <= 2 waves per SIMD
   if (occ > by_waves) occ = by_waves;
@@ -594,18 +805,23 @@ int damd_conv_default_cfg(int K, int64_t M) {
   return 2;
 }
 
-int damd_conv_supported(int C, int K, int cfg) {
+// W: input width (the halo configs stage BP + 2W + 2 pixel rows per channel block)
+int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, int cfg) {
   if (cfg < 0 || cfg >= kNumCfgs) return 0;
-  return C % kBK == 0 && C > 0 && K % kCfgs[cfg].bco == 0;
+  const Cfg c = kCfgs[cfg];
+  if (!(C % kBK == 0 && C > 0 && K % c.bco == 0)) return 0;
+  if (c.nst == 0)
+    return R == 3 && S == 3 && stride == 1 && pad == 1 && W >= 1 && halo_lds_bytes(c, W) <= kHaloMaxLds;
+  return 1;
 }
 
 // groups (pixel-tile strides) for a config; also the leading dim of the stats partials
-int damd_conv_groups(int64_t M, int K, int cfg, int groups_override) {
+int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
   const Cfg c = kCfgs[cfg];
   const int64_t ptiles = (M + c.bp - 1) / c.bp;
   const int ctiles = K / c.bco;
   int64_t groups = groups_override > 0 ? groups_override
-                                       : (256LL * blocks_per_cu(c) + ctiles - 1) / ctiles;
+                                       : (256LL * blocks_per_cu(c, W) + ctiles - 1) / ctiles;
   if (groups > ptiles) groups = ptiles;
   if (groups < 1) groups = 1;
   return static_cast<int>(groups);
@@ -618,7 +834,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi,
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
                          const float* scale, const float* shift) {
-  if (!damd_conv_supported(C, K, cfg)) return -1;
+  if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
   if (epi < 0 || epi > 3 || (epi != 0 && part == nullptr)) return -3;
   if (epi >= 2 && (yb == nullptr || mean == nullptr || (epi == 2 && mask == nullptr) ||
                    (epi == 3 && (scale == nullptr || shift == nullptr))))
@@ -650,16 +866,39 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
       default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR); break; \
     }                                                     \
   } while (0)
+  const int HR = halo_rows(c.bp, W);
+  const int hlds = c.nst == 0 ? halo_lds_bytes(c, W) : 0;
+#define H1(BCO, BP, WCO, NW, E)                                                                              \
+  do {                                                                                                       \
+    auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E>;                                                          \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR);                       \
+  } while (0)
+#define H(BCO, BP, WCO, NW)                              \
+  do {                                                   \
+    switch (epi) {                                       \
+      case 0: H1(BCO, BP, WCO, NW, kEpiNone); break;     \
+      case 1: H1(BCO, BP, WCO, NW, kEpiStats); break;    \
+      case 2: H1(BCO, BP, WCO, NW, kEpiBnbM); break;     \
+      default: H1(BCO, BP, WCO, NW, kEpiBnbR); break;    \
+    }                                                    \
+  } while (0)
   switch (cfg) {
     case 0: L(64, 128, 1, 4, 2); break;
     case 1: L(128, 128, 2, 4, 2); break;
     case 2: L(64, 256, 1, 4, 2); break;
     case 3: L(128, 256, 2, 8, 3); break;
     case 4: L(64, 256, 1, 8, 3); break;
-    default: L(256, 128, 4, 8, 3); break;
+    case 5: L(256, 128, 4, 8, 3); break;
+    case 6: H(128, 256, 2, 8); break;
+    case 7: H(64, 256, 1, 8); break;
+    case 8: H(128, 128, 2, 4); break;
+    default: H(256, 128, 4, 8); break;
   }
 #undef L
 #undef L1
+#undef H
+#undef H1
   DAMD_CHECK_LAUNCH();
   return 0;
 }

@@ -120,8 +120,8 @@ def tuned_choices() -> Dict[tuple, object]:
     return dict(_TUNE)
 
 
-def _igemm_cfgs(ext, x: torch.Tensor, w: torch.Tensor):
-    return [c for c in range(ext.conv_num_cfgs()) if ext.conv_supported(x, w, c)]
+def _igemm_cfgs(ext, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int):
+    return [c for c in range(ext.conv_num_cfgs()) if ext.conv_supported(x, w, c, stride, pad)]
 
 
 def _flip_weight(w: torch.Tensor) -> torch.Tensor:
@@ -144,7 +144,7 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
         return miopen()
     wt = _flip_weight(w)
     cands: Dict[object, Callable[[], object]] = {}
-    for c in _igemm_cfgs(e, dy, wt):
+    for c in _igemm_cfgs(e, dy, wt, 1, k - 1 - pad):
         cands[c] = (lambda c=c: e.conv_fwd(dy, wt, 1, k - 1 - pad, False, c, 0)[0])
     cands["miopen"] = miopen
     if k == 1:
@@ -217,7 +217,8 @@ def igemm_fusable(conv: nn.Module, x: torch.Tensor) -> bool:
         return False
     from determined_amd import ops
 
-    return ops.fusion_enabled("igemm_conv") and bool(ops.ext().conv_supported(x, conv.weight, -1))
+    return ops.fusion_enabled("igemm_conv") and bool(ops.ext().conv_supported(x, conv.weight, -1, conv.stride[0],
+                                                                              conv.padding[0]))
 
 
 def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -233,7 +234,7 @@ def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple
     st, pad = conv.stride[0], conv.padding[0]
     w = conv.weight
     key = ("fwd", tuple(x.shape), tuple(w.shape), st, pad)
-    cands = {c: (lambda c=c: e.conv_fwd(x, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, x, w)}
+    cands = {c: (lambda c=c: e.conv_fwd(x, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, x, w, st, pad)}
     cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
     stats = stats and ops.fusion_enabled("conv_stats")
     y, part = _IGemmConvFn.apply(x, w, st, pad, stats, cfg)
@@ -288,10 +289,11 @@ class _BNActConvFn(torch.autograd.Function):
         g_a = None if g_a is None else g_a.contiguous(memory_format=cl)
         dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
         wt = _flip_weight(conv_w) if stride == 1 and 2 * pad == k - 1 else None
-        fused = wt is not None and (mask is not None or not has_res) and bool(e.conv_supported(g_z, wt, -1))
+        fused = (wt is not None and (mask is not None or not has_res)
+                 and bool(e.conv_supported(g_z, wt, -1, 1, k - 1 - pad)))
         if fused:
             cands = {c: (lambda c=c: e.conv_dgrad_bn(g_z, wt, k - 1 - pad, c, g_a, y, mask, stats))
-                     for c in _igemm_cfgs(e, g_z, wt)}
+                     for c in _igemm_cfgs(e, g_z, wt, 1, k - 1 - pad)}
             key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
             dz, part = cands[_pick(key, cands, default=e.conv_default_cfg(wt.shape[0]))]()
             dy, dg, db = e.bn_bwd_from_part(dz, y, stats, bn_w, part)
@@ -322,7 +324,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
         cfg = _TUNE.get(key)
         if cfg is None:  # tune the conv on a stand-in input of the same shape
-            cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w)}
+            cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w, st, pad)}
             cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
         return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,
                                   cfg)

@@ -77,7 +77,7 @@ def main():
         ref = F.conv2d(xs.float(), w.float(), stride=st, padding=pad)
         errs = {}
         for cfg in range(ncfg):
-            if not e.conv_supported(xs, w, cfg):
+            if not e.conv_supported(xs, w, cfg, st, pad):
                 continue
             y, part = e.conv_fwd(xs, w, st, pad, True, cfg, 0)
             err = ((y.float() - ref).norm() / ref.norm()).item()
@@ -114,7 +114,7 @@ def main():
             rec["miopen_dgrad_us"] = round(timeit(miopen_dgrad), 1)
             rec["ours_dgrad_us"] = {}
             for cfg in range(ncfg):
-                if e.conv_supported(dy, wt, cfg):
+                if e.conv_supported(dy, wt, cfg, 1, k - 1 - pad):
                     rec["ours_dgrad_us"][str(cfg)] = round(timeit(lambda: e.conv_fwd(dy, wt, 1, k - 1 - pad, False, cfg, 0)), 1)
             if rec["ours_dgrad_us"]:
                 tot["miopen_dgrad"] += rec["miopen_dgrad_us"] * cnt

@@ -24,6 +24,8 @@ SHAPES = [  # (n, cin, cout, k, stride, hw)
     (2, 128, 64, 3, 2, 11),
     (1, 256, 256, 1, 2, 14),
     (2, 192, 128, 3, 1, 5),
+    (2, 64, 64, 3, 1, 30),
+    (1, 128, 256, 3, 1, 57),
 ]
 
 
@@ -36,7 +38,7 @@ def test_conv_fwd_and_stats_match_fp32(ext, shape):
     w = cl((torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).to(torch.bfloat16))
     ref = F.conv2d(x.float(), w.float(), stride=st, padding=pad)
     for cfg in range(ext.conv_num_cfgs()):
-        if not ext.conv_supported(x, w, cfg):
+        if not ext.conv_supported(x, w, cfg, st, pad):
             continue
         y, part = ext.conv_fwd(x, w, st, pad, True, cfg, 0)
         assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
@@ -60,7 +62,7 @@ def test_conv_dgrad_via_flipped_weights(ext, shape):
     dy = cl(torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16))
     ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), stride=1, padding=pad)
     wt = cl(w.flip(2, 3).transpose(0, 1))
-    if not ext.conv_supported(dy, wt, -1):
+    if not ext.conv_supported(dy, wt, -1, 1, k - 1 - pad):
         pytest.skip("channel count not covered by a config")
     dx, _ = ext.conv_fwd(dy, wt, 1, k - 1 - pad, False, -1, 0)
     torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())

@@ -427,16 +427,19 @@ def test_conv_dgrad_bn_epilogue(ops, k, masked, with_d2):
     assert (mask.numel() > 0) == masked
     d2 = torch.randn_like(yb) if with_d2 else None
     wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)
-    dz, part = e.conv_dgrad_bn(g, wt, k // 2, -1, d2, yb, mask if masked else None, stats)
     da = torch.nn.grad.conv2d_input(yb.shape, w.float(), g.float(), padding=k // 2)
     if with_d2:
         da = da + d2.float()
     ref = da * (a.float() > 0)
-    torch.testing.assert_close(dz.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
-    dzf = dz.float()
-    torch.testing.assert_close(part[:, 0].sum(0), dzf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
     cen = yb.float() - stats[0].view(1, -1, 1, 1)
-    torch.testing.assert_close(part[:, 1].sum(0), (dzf * cen).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_supported(g, wt, c, 1, k // 2)]
+    assert cfgs
+    for cfg in cfgs:  # generic and (3x3) halo kernels
+        dz, part = e.conv_dgrad_bn(g, wt, k // 2, cfg, d2, yb, mask if masked else None, stats)
+        torch.testing.assert_close(dz.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        dzf = dz.float()
+        torch.testing.assert_close(part[:, 0].sum(0), dzf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(part[:, 1].sum(0), (dzf * cen).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("depth", [3])
