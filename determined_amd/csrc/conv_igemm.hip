@@ -176,12 +176,11 @@ __device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t 
         }
         if (ok) {
           *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
-          if (EPI == kEpiStats) {
+          if (EPI == kEpiStats) {  // statistics of the fp32 conv outputs (before the bf16 store)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float f = bf2f(v.v[e]);
-              st_s[q][e] += f;
-              st_q[q][e] += f * f;
+              st_s[q][e] += o[e];
+              st_q[q][e] += o[e] * o[e];
             }
           } else if (EPI >= kEpiBnbM) {
             const float4 u0 = *reinterpret_cast<const float4*>(prm + cl);
@@ -292,46 +291,50 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     const int co = 8 * (wave + NW * i) + prow;
     wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
   }
-  // pixel rows: per tile (image offset + chunk, top-left input coordinate, validity)
-  int64_t xoff[NIX];
-  int ih0[NIX], iw0[NIX];
+  // pixel rows, per tile: element offset of the row's tap-(0,0) input pixel (+ its DMA chunk;
+  // may lie outside the image -- only dereferenced for valid taps) and a bit mask of the taps
+  // r*S + s that fall inside the image.  Per k-step the source is then one 64-bit add of a
+  // wave-uniform tap/channel offset and a bit test (the per-k-step im2col arithmetic was ~4
+  // VALU instructions per MFMA in the PMC counters).
+  int64_t xbase[NIX];
+  uint32_t vmask[NIX];
   const int OHW = g.OH * g.OW;
   auto tile_rows = [&](int pt) {
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
       const int p = 8 * (wave + NW * i) + prow;
       const int m = pt * BP + p;  // M < 2^31 (host-checked)
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
+      const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
+      xbase[i] = ((static_cast<int64_t>(n) * g.H + ih0) * g.W + iw0) * g.C + ((slot ^ swz(p)) << 3);
+      uint32_t bits = 0;
       if (m < g.M) {
-        const int n = m / OHW;
-        const int rem = m - n * OHW;
-        const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
-        ih0[i] = oh * g.stride - g.pad;
-        iw0[i] = ow * g.stride - g.pad;
-        xoff[i] = static_cast<int64_t>(n) * g.H * g.W * g.C + ((slot ^ swz(p)) << 3);
-      } else {
-        ih0[i] = -0x40000000;  // never in range
-        iw0[i] = 0;
-        xoff[i] = 0;
+        for (int r = 0; r < g.R; ++r) {
+          const bool rok = static_cast<unsigned>(ih0 + r) < static_cast<unsigned>(g.H);
+          for (int s2 = 0; s2 < g.S; ++s2)
+            if (rok && static_cast<unsigned>(iw0 + s2) < static_cast<unsigned>(g.W)) bits |= 1u << (r * g.S + s2);
+        }
       }
+      vmask[i] = bits;
     }
   };
 
-  // load-side counters: tile, channel block, tap (r, s)
+  // load-side counters: tile, channel block, tap (r, s), k-step
   int l_tile = 0, l_cb = 0, l_r = 0, l_s = 0, l_ks = 0;
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
   auto issue = [&](int stage) {
     bf16_t* sw = lds + stage * STAGE;
     const int pt = grp + l_tile * g.groups;
     if (l_ks == 0) tile_rows(pt);
 #pragma unroll
     for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + NW * i) * kBK);
-    const int c0 = l_cb * kBK;
+    const int tap = l_r * g.S + l_s;
+    const int64_t soff = static_cast<int64_t>(l_r * g.W + l_s) * g.C + l_cb * kBK;  // wave-uniform
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
-      const int ih = ih0[i] + l_r, iw = iw0[i] + l_s;
-      const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
-      const bf16_t* src = ok ? x + xoff[i] + (static_cast<int64_t>(ih) * g.W + iw) * g.C + c0
-                             : reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+      const bf16_t* src = (vmask[i] >> tap) & 1u ? x + (xbase[i] + soff) : zero;
       dma16(src, sw + (BCO + 8 * (wave + NW * i)) * kBK);
     }
     // advance (cb fastest, then s, then r, then tile)
@@ -344,6 +347,23 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
     if (++l_ks == g.ksteps) { l_ks = 0; ++l_tile; }
   };
+
+  // per-lane LDS fragment offsets (elements) for the two 32-deep k halves of a stage
+  int aoff[2][FI], boff[2][FJ];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int chunk = kk * 4 + lg;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wco0 + a_row(i, rho);
+      aoff[kk][i] = row * kBK + ((chunk ^ swz(row)) << 3);
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int row = wp0 + 16 * j + rho;
+      boff[kk][j] = (BCO + row) * kBK + ((chunk ^ swz(row)) << 3);
+    }
+  }
 
   f4 acc[FI][FJ];
 #pragma unroll
@@ -371,21 +391,13 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
     if (it + NST - 1 < items) issue((it + NST - 1) % NST);
     const bf16_t* sw = lds + (it % NST) * STAGE;
-    const bf16_t* sx = sw + BCO * kBK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + lg;
       s8 a[FI], b[FJ];
 #pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        const int row = wco0 + a_row(i, rho);
-        a[i] = *reinterpret_cast<const s8*>(sw + row * kBK + ((chunk ^ swz(row)) << 3));
-      }
+      for (int i = 0; i < FI; ++i) a[i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        const int row = wp0 + 16 * j + rho;
-        b[j] = *reinterpret_cast<const s8*>(sx + row * kBK + ((chunk ^ swz(row)) << 3));
-      }
+      for (int j = 0; j < FJ; ++j) b[j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -809,7 +821,7 @@ int damd_conv_default_cfg(int K, int64_t M) {
 int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, int cfg) {
   if (cfg < 0 || cfg >= kNumCfgs) return 0;
   const Cfg c = kCfgs[cfg];
-  if (!(C % kBK == 0 && C > 0 && K % c.bco == 0)) return 0;
+  if (!(C % kBK == 0 && C > 0 && K % c.bco == 0 && R * S <= 32)) return 0;
   if (c.nst == 0)
     return R == 3 && S == 3 && stride == 1 && pad == 1 && W >= 1 && halo_lds_bytes(c, W) <= kHaloMaxLds;
   return 1;

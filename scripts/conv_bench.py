@@ -81,9 +81,8 @@ def main():
                 continue
             y, part = e.conv_fwd(xs, w, st, pad, True, cfg, 0)
             err = ((y.float() - ref).norm() / ref.norm()).item()
-            yf = y.float()
-            ssum = yf.sum((0, 2, 3))
-            ssq = (yf * yf).sum((0, 2, 3))
+            ssum = ref.sum((0, 2, 3))  # the epilogue sums the fp32 outputs
+            ssq = (ref * ref).sum((0, 2, 3))
             serr = max(((part[:, 0].sum(0) - ssum).abs().max() / ssum.abs().max().clamp_min(1e-3)).item(),
                        ((part[:, 1].sum(0) - ssq).abs().max() / ssq.abs().max()).item())
             errs[cfg] = (round(err, 5), round(serr, 6))

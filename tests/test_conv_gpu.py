@@ -43,9 +43,11 @@ def test_conv_fwd_and_stats_match_fp32(ext, shape):
         y, part = ext.conv_fwd(x, w, st, pad, True, cfg, 0)
         assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
         torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
-        yf = y.float()
-        torch.testing.assert_close(part[:, 0].sum(0), yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
-        torch.testing.assert_close(part[:, 1].sum(0), (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        # statistics of the fp32 conv outputs (before the bf16 store)
+        tol = 2e-3 * ref.abs().sum((0, 2, 3)).max().item()
+        torch.testing.assert_close(part[:, 0].sum(0), ref.sum((0, 2, 3)), rtol=1e-3, atol=tol)
+        torch.testing.assert_close(part[:, 1].sum(0), (ref * ref).sum((0, 2, 3)), rtol=2e-3,
+                                   atol=2e-3 * (ref * ref).sum((0, 2, 3)).max().item())
         # a forced small group count exercises several pixel tiles per block (persistent loop)
         y2, _ = ext.conv_fwd(x, w, st, pad, False, cfg, 1)
         torch.testing.assert_close(y2, y, rtol=0, atol=0)
