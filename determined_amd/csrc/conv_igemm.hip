@@ -240,7 +240,10 @@ __device__ __forceinline__ void epi_flush_sums(float (&st_s)[FI / 2][8], float (
 }
 
 
-template <int BCO, int BP, int WCO, int NW, int NST, int EPI>
+// SCH (k-step schedule): 0 = per 32-deep half: fragment reads then its MFMAs; 1 = all fragment
+// reads of the k-step issued first (the second half's reads overlap the first half's MFMAs);
+// 2 = as 1 with s_setprio(1) over the MFMA block.
+template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                 float* __restrict__ part, Geo g, EpiArgs ea) {
@@ -391,17 +394,36 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
     if (it + NST - 1 < items) issue((it + NST - 1) % NST);
     const bf16_t* sw = lds + (it % NST) * STAGE;
+    if (SCH == 0) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      s8 a[FI], b[FJ];
+      for (int kk = 0; kk < 2; ++kk) {
+        s8 a[FI], b[FJ];
 #pragma unroll
-      for (int i = 0; i < FI; ++i) a[i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
+        for (int i = 0; i < FI; ++i) a[i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) b[j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
+        for (int j = 0; j < FJ; ++j) b[j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
 #pragma unroll
-      for (int i = 0; i < FI; ++i)
+        for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+      }
+    } else {
+      s8 a[2][FI], b[2][FJ];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < FI; ++i) a[kk][i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) b[kk][j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
+      }
+      if (SCH == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
+      if (SCH == 2) __builtin_amdgcn_s_setprio(0);
     }
     if (++c_ks == g.ksteps) {
       epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, grp + static_cast<int64_t>(c_tile) * g.groups, ct, wco0, wp0, lg, rho,
@@ -778,15 +800,16 @@ using namespace damd::igemm;
 namespace {
 
 struct Cfg {
-  int bco, bp, wco, nw, nst;
+  int bco, bp, wco, nw, nst, sch;
 };
 // 0-2: 4 waves, 2-slot ring; 3-5: 8 waves, 3-slot ring (the tiles that won on some ResNet-50
 // layer in profiles/conv_igemm_*; 128x256 / 256x128 with 4 waves spill and never won)
 // nst = 0 marks the 3x3 halo kernel (stride-1 3x3 only)
-constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2},  {128, 128, 2, 4, 2}, {64, 256, 1, 4, 2},
-                         {128, 256, 2, 8, 3}, {64, 256, 1, 8, 3},  {256, 128, 4, 8, 3},
-                         {128, 256, 2, 8, 0}, {64, 256, 1, 8, 0},  {128, 128, 2, 4, 0},
-                         {256, 128, 4, 8, 0}};
+constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2, 0},  {128, 128, 2, 4, 2, 0}, {64, 256, 1, 4, 2, 0},
+                         {128, 256, 2, 8, 3, 0}, {64, 256, 1, 8, 3, 0},  {256, 128, 4, 8, 3, 0},
+                         {128, 256, 2, 8, 0, 0}, {64, 256, 1, 8, 0, 0},  {128, 128, 2, 4, 0, 0},
+                         {256, 128, 4, 8, 0, 0}, {128, 128, 2, 4, 2, 1}, {256, 128, 4, 8, 3, 1},
+                         {128, 128, 2, 4, 2, 2}, {256, 128, 4, 8, 3, 2}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
@@ -867,17 +890,18 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
-#define L1(BCO, BP, WCO, NW, NST, E) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea)
-#define L(BCO, BP, WCO, NW, NST)                          \
-  do {                                                    \
-    switch (epi) {                                        \
-      case 0: L1(BCO, BP, WCO, NW, NST, kEpiNone); break;  \
-      case 1: L1(BCO, BP, WCO, NW, NST, kEpiStats); break; \
-      case 2: L1(BCO, BP, WCO, NW, NST, kEpiBnbM); break;  \
-      default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR); break; \
-    }                                                     \
+#define L1(BCO, BP, WCO, NW, NST, E, SC) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea)
+#define LS(BCO, BP, WCO, NW, NST, SC)                          \
+  do {                                                         \
+    switch (epi) {                                             \
+      case 0: L1(BCO, BP, WCO, NW, NST, kEpiNone, SC); break;  \
+      case 1: L1(BCO, BP, WCO, NW, NST, kEpiStats, SC); break; \
+      case 2: L1(BCO, BP, WCO, NW, NST, kEpiBnbM, SC); break;  \
+      default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR, SC); break; \
+    }                                                          \
   } while (0)
+#define L(BCO, BP, WCO, NW, NST) LS(BCO, BP, WCO, NW, NST, 0)
   const int HR = halo_rows(c.bp, W);
   const int hlds = c.nst == 0 ? halo_lds_bytes(c, W) : 0;
 #define H1(BCO, BP, WCO, NW, E)                                                                              \
@@ -905,9 +929,14 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
     case 6: H(128, 256, 2, 8); break;
     case 7: H(64, 256, 1, 8); break;
     case 8: H(128, 128, 2, 4); break;
-    default: H(256, 128, 4, 8); break;
+    case 9: H(256, 128, 4, 8); break;
+    case 10: LS(128, 128, 2, 4, 2, 1); break;
+    case 11: LS(256, 128, 4, 8, 3, 1); break;
+    case 12: LS(128, 128, 2, 4, 2, 2); break;
+    default: LS(256, 128, 4, 8, 3, 2); break;
   }
 #undef L
+#undef LS
 #undef L1
 #undef H
 #undef H1
