@@ -68,13 +68,17 @@ extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, i
                                  int, int, int, hipStream_t);
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
-                                    const float*, const float*, const float*);
+                                    const float*, const float*, const float*, int, const void*, const float*,
+                                    const float*, void*, uint8_t*);
+extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
                         float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*, const float*, int);
 void damd_bn_bwd_from_part_launch(const void*, const void*, int64_t, int, const float*, const float*, const float*,
                                   const float*, int, float*, void*, void*, void*, int, int, hipStream_t);
+void damd_bn_finalize_launch(const float*, int, int, int64_t, const void*, const void*, float*, float*, float, float,
+                             float*, float*, float*, float*, int, hipStream_t);
 void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
                                hipStream_t);
 void damd_bn_bwd_launch(const void*, const void*, const void*, int64_t, int, const float*, const float*,
@@ -444,6 +448,32 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// BN forward statistics (mean, invstd, scale, shift) [4, C] from producer partials [nb, 2, C]
+// of a tensor with M rows; updates the running statistics.
+at::Tensor bn_finalize_part(const at::Tensor& part, int64_t M, const at::Tensor& weight, const at::Tensor& bias,
+                            const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+                            double momentum, double eps) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 3 && part.size(1) == 2 &&
+              part.is_contiguous(), "bn_finalize_part: part must be float32 [nb, 2, C]");
+  const int64_t C = part.size(2);
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C && weight.scalar_type() == bias.scalar_type(),
+              "bn_finalize_part: weight/bias must have C elements");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    TORCH_CHECK(running_mean->scalar_type() == at::kFloat && running_var->scalar_type() == at::kFloat,
+                "running stats must be float32");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  auto stats = at::empty({4, C}, part.options());
+  damd_bn_finalize_launch(part.data_ptr<float>(), static_cast<int>(part.size(0)), static_cast<int>(C), M,
+                          weight.data_ptr(), bias.data_ptr(), rm, rv, static_cast<float>(momentum),
+                          static_cast<float>(eps), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
+                          stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), dtype_code(weight), cur_stream());
+  return stats;
+}
+
 // BN backward from producer-computed reduce partials (conv_dgrad_bn): dz already carries the
 // ReLU mask; returns (dx, dgamma, dbeta).
 std::vector<at::Tensor> bn_bwd_from_part(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& stats,
@@ -695,9 +725,51 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
-                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr);
   TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
   return {y, part};
+}
+
+// z = conv1x1(a, w) with a = relu(y * stats[2] + stats[3] [+ res]) computed inside the conv's
+// operand staging (ProArgs); returns (z, z's BN statistic partials [groups, 2, K], a, a's ReLU bit
+// mask or an empty tensor).  stats: [4, C] of y's BatchNorm (mean, invstd, scale, shift).
+std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w, const c10::optional<at::Tensor>& res,
+                                       const at::Tensor& stats, bool want_mask, int64_t cfg) {
+  TORCH_CHECK(conv_supported(y, w, cfg, 1, 0) && w.size(2) == 1 && w.size(3) == 1, "conv_bnact_fwd: unsupported input");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3), K = w.size(0);
+  TORCH_CHECK(damd_conv_pro_supported(static_cast<int>(C), static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg)),
+              "conv_bnact_fwd: config has no prologue variant");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(0) == 4 && stats.size(1) == C &&
+              stats.is_contiguous(), "conv_bnact_fwd: stats must be float32 [4, C]");
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    TORCH_CHECK(res->sizes() == y.sizes() && res->strides() == y.strides() && res->scalar_type() == y.scalar_type(),
+                "conv_bnact_fwd: res must match y");
+    rp = res->data_ptr();
+  }
+  const int64_t M = N * H * W;
+  TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_bnact_fwd: tensor too large");
+  auto wl = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto z = at::empty({N, K, H, W}, y.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = at::empty_like(y);
+  auto mask = want_mask ? at::empty({M * C / 8}, y.options().dtype(at::kByte)) : at::empty({0}, y.options().dtype(at::kByte));
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
+  auto part = at::empty({G, 2, K}, y.options().dtype(at::kFloat));
+  const int rc = damd_conv_fwd_launch(y.data_ptr(), wl.data_ptr(), z.data_ptr(), part.data_ptr<float>(),
+                                      static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                      static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 1,
+                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
+                                      stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), a.data_ptr(),
+                                      want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+  TORCH_CHECK(rc == 0, "conv_bnact_fwd: launch rejected");
+  return {z, part, a, mask};
+}
+
+bool conv_pro_supported(const at::Tensor& y, const at::Tensor& w, int64_t cfg) {
+  return conv_supported(y, w, cfg, 1, 0) && w.size(2) == 1 && w.size(3) == 1 &&
+         damd_conv_pro_supported(static_cast<int>(y.size(1)), static_cast<int>(w.size(0)), 1, 1, 1, 0,
+                                 static_cast<int>(cfg));
 }
 
 // Stride-1 input gradient dX = conv(dY, wt, pad) (wt = flipped, transposed weights) of a conv
@@ -742,7 +814,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
                                       yb.data_ptr(), mp, stats[0].data_ptr<float>(), stats[2].data_ptr<float>(),
-                                      stats[3].data_ptr<float>());
+                                      stats[3].data_ptr<float>(), 0, nullptr, nullptr, nullptr, nullptr, nullptr);
   TORCH_CHECK(rc == 0, "conv_dgrad_bn: launch rejected");
   return {dz, part};
 }
@@ -944,6 +1016,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("bn_bwd_from_part", &bn_bwd_from_part);
+  m.def("bn_finalize_part", &bn_finalize_part);
   m.def("bn_apply", &bn_apply);
   m.def("bn_pool_fwd", &bn_pool_fwd);
   m.def("resid_norm_supported", &resid_norm_supported);
@@ -954,6 +1027,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_supported", &conv_supported);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
+  m.def("conv_bnact_fwd", &conv_bnact_fwd);
+  m.def("conv_pro_supported", &conv_pro_supported);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
   m.def("wgrad_supported", &wgrad_supported);

@@ -767,6 +767,24 @@ void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int 
   DAMD_CHECK_LAUNCH();
 }
 
+// BN forward statistics from producer partials only (no apply pass): mean / invstd / folded
+// scale and shift + running-statistics update, for a consumer that applies the BN itself
+// (conv_igemm.hip prologue mode).
+void damd_bn_finalize_launch(const float* part, int nb, int C, int64_t M, const void* w, const void* b,
+                             float* run_mean, float* run_var, float momentum, float eps, float* mean, float* invstd,
+                             float* scale, float* shift, int w_dtype, hipStream_t st) {
+  const dim3 fg((C + kFinCh - 1) / kFinCh);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
+                       eps, static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd,
+                       scale, shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
+                       eps, static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd,
+                       scale, shift);
+  DAMD_CHECK_LAUNCH();
+}
+
 void damd_bn_apply_only_launch(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                                const float* shift, int relu, int x_dtype, hipStream_t st) {
   const int TPR = C / 8;

@@ -105,6 +105,20 @@ struct EpiArgs {
 
 // Tile epilogue shared by the conv kernels (EPI modes above): stores the BP x BCO output tile of
 // pixel tile pt / co tile ct from the accumulators, accumulating the per-lane channel sums.
+// Prologue (PRO) mode of the generic kernel, 1x1 / stride 1 only: the input operand is
+// a = relu(y * scale[c] + shift[c] [+ res]) computed while staging (global -> registers ->
+// transform -> LDS) instead of read from a materialised `a`; the blocks of co tile 0 also write
+// `a` (aout) and its ReLU bit mask (mout) for the backward / the shortcut consumer.  This fuses
+// a BatchNorm(+residual)+ReLU forward apply pass into its consuming 1x1 convolution: the
+// activation is read as (y, res) once instead of (y, res) by the BN pass and `a` by the conv.
+struct ProArgs {
+  const bf16_t* res;     // residual added before the ReLU, or null
+  const float* scale;    // folded BN scale / shift of the input channels [C]
+  const float* shift;
+  bf16_t* aout;          // a, [M][C], or null
+  uint8_t* mout;         // ReLU bit mask of a, [M][C/8], or null
+};
+
 template <int BCO, int BP, int FI, int FJ, int EPI>
 __device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t pt, int ct, int wco0, int wp0, int lg,
                                                int rho, const Geo& g, const EpiArgs& ea, const float* prm,
@@ -243,10 +257,10 @@ __device__ __forceinline__ void epi_flush_sums(float (&st_s)[FI / 2][8], float (
 // SCH (k-step schedule): 0 = per 32-deep half: fragment reads then its MFMAs; 1 = all fragment
 // reads of the k-step issued first (the second half's reads overlap the first half's MFMAs);
 // 2 = as 1 with s_setprio(1) over the MFMA block.
-template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0>
+template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0, int PRO = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-                float* __restrict__ part, Geo g, EpiArgs ea) {
+                float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -258,6 +272,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   constexpr int NIW = BCO / (8 * NW), NIX = BP / (8 * NW);  // DMA instructions per wave per stage
   constexpr int NL = NIW + NIX;
   static_assert(NL * (NST - 2) <= 63, "vmcnt range");
+  static_assert(!PRO || (NST == 3 && SCH == 0), "prologue mode uses the 3-slot ring");
   // one LDS array (a second __shared__ object makes hipcc wait for every DMA before each
   // ds_read): NST ring slots, then the block's per-channel BN parameters for the BN-backward
   // epilogues (mean, scale, shift of its BCO output channels; the co tile is fixed per block)
@@ -324,21 +339,81 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
   };
 
+  // PRO: register-staged input rows of one k-step (lane: channel chunk `slot`, rows
+  // 8 * (wave + NW * i) + prow), their BN parameters, and the tile / channel block they belong to
+  bf16x8 py[PRO ? NIX : 1], pr[PRO ? NIX : 1];
+  float4 psc[2], psh[2];
+  int p_pt = 0, p_cb = 0;
+  auto load_px = [&](int pt, int cb) {
+    p_pt = pt;
+    p_cb = cb;
+    const int cofs = cb * kBK + (slot << 3);
+#pragma unroll
+    for (int i = 0; i < NIX; ++i) {
+      const int m = pt * BP + 8 * (wave + NW * i) + prow;
+      const int64_t off = static_cast<int64_t>(m < g.M ? m : 0) * g.C + cofs;
+      py[i] = *reinterpret_cast<const bf16x8*>(x + off);
+      if (pa.res != nullptr) pr[i] = *reinterpret_cast<const bf16x8*>(pa.res + off);
+    }
+    psc[0] = *reinterpret_cast<const float4*>(pa.scale + cofs);
+    psc[1] = *reinterpret_cast<const float4*>(pa.scale + cofs + 4);
+    psh[0] = *reinterpret_cast<const float4*>(pa.shift + cofs);
+    psh[1] = *reinterpret_cast<const float4*>(pa.shift + cofs + 4);
+  };
+  // transform the staged rows into LDS slot `stage` (+ a / mask stores by co tile 0)
+  auto store_px = [&](int stage) {
+    bf16_t* sx = lds + stage * STAGE + BCO * kBK;
+    const float sc[8] = {psc[0].x, psc[0].y, psc[0].z, psc[0].w, psc[1].x, psc[1].y, psc[1].z, psc[1].w};
+    const float sh[8] = {psh[0].x, psh[0].y, psh[0].z, psh[0].w, psh[1].x, psh[1].y, psh[1].z, psh[1].w};
+    const bool has_res = pa.res != nullptr;
+#pragma unroll
+    for (int i = 0; i < NIX; ++i) {
+      const int row = 8 * (wave + NW * i) + prow;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = bf2f(py[i].v[e]) * sc[e] + sh[e];
+        if (has_res) t += bf2f(pr[i].v[e]);
+        v[e] = fmaxf(t, 0.f);
+      }
+      bf16x8 o;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const u16v2_t pk = f2bf2(v[e], v[e + 1]);
+        o.v[e] = pk[0]; o.v[e + 1] = pk[1];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= (v[e] > 0.f ? 1u : 0u) << e;
+      *reinterpret_cast<bf16x8*>(sx + row * kBK + ((slot ^ swz(row)) << 3)) = o;
+      const int m = p_pt * BP + row;
+      if (ct == 0 && m < g.M) {
+        const int64_t off = static_cast<int64_t>(m) * g.C + p_cb * kBK + (slot << 3);
+        if (pa.aout != nullptr) *reinterpret_cast<bf16x8*>(pa.aout + off) = o;
+        if (pa.mout != nullptr) pa.mout[off >> 3] = static_cast<uint8_t>(bits);
+      }
+    }
+  };
+
   // load-side counters: tile, channel block, tap (r, s), k-step
   int l_tile = 0, l_cb = 0, l_r = 0, l_s = 0, l_ks = 0;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
   auto issue = [&](int stage) {
     bf16_t* sw = lds + stage * STAGE;
     const int pt = grp + l_tile * g.groups;
-    if (l_ks == 0) tile_rows(pt);
+    if (!PRO && l_ks == 0) tile_rows(pt);
 #pragma unroll
     for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + NW * i) * kBK);
-    const int tap = l_r * g.S + l_s;
-    const int64_t soff = static_cast<int64_t>(l_r * g.W + l_s) * g.C + l_cb * kBK;  // wave-uniform
+    if (!PRO) {
+      const int tap = l_r * g.S + l_s;
+      const int64_t soff = static_cast<int64_t>(l_r * g.W + l_s) * g.C + l_cb * kBK;  // wave-uniform
 #pragma unroll
-    for (int i = 0; i < NIX; ++i) {
-      const bf16_t* src = (vmask[i] >> tap) & 1u ? x + (xbase[i] + soff) : zero;
-      dma16(src, sw + (BCO + 8 * (wave + NW * i)) * kBK);
+      for (int i = 0; i < NIX; ++i) {
+        const bf16_t* src = (vmask[i] >> tap) & 1u ? x + (xbase[i] + soff) : zero;
+        dma16(src, sw + (BCO + 8 * (wave + NW * i)) * kBK);
+      }
+    } else {
+      load_px(pt, l_cb);
     }
     // advance (cb fastest, then s, then r, then tile)
     if (++l_cb == g.cblk) {
@@ -381,18 +456,37 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
   }
 
+  if (PRO) {
+    // item j: weights DMA + input rows to registers at iteration j-2, transform into LDS at
+    // iteration j-1, MFMAs at iteration j
+    if (items > 0) {
+      issue(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_px(0);
+    }
+    if (items > 1) issue(1);
+  } else {
 #pragma unroll
-  for (int s0 = 0; s0 < NST - 1; ++s0)
-    if (s0 < items) issue(s0);
+    for (int s0 = 0; s0 < NST - 1; ++s0)
+      if (s0 < items) issue(s0);
+  }
   int c_ks = 0, c_tile = 0;
   for (int it = 0; it < items; ++it) {
-    // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
-    const int ahead = items - 1 - it;
-    if (NST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
-    else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
-    if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+    if (PRO) {
+      // weights of item it, input registers of item it+1 and this wave's LDS writes of item it
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (it + 1 < items) store_px((it + 1) % NST);
+      if (it + 2 < items) issue((it + 2) % NST);
+    } else {
+      // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
+      const int ahead = items - 1 - it;
+      if (NST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
+      else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
+      if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+    }
     const bf16_t* sw = lds + (it % NST) * STAGE;
     if (SCH == 0) {
 #pragma unroll
@@ -865,11 +959,23 @@ int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
 // x: [N, H, W, C] bf16; w: [K, R, S, C] bf16; y: [N, OH, OW, K] bf16;
 // part: null or [groups][2][K] fp32 (epi 1: sum / sum of squares of y; epi 2, 3: see EpiArgs)
 // epi: 0 none, 1 stats, 2 BN-backward with bit mask, 3 BN-backward with recomputed ReLU mask
+int damd_conv_pro_supported(int C, int K, int R, int S, int stride, int pad, int cfg) {
+  if (cfg < 0 || cfg >= kNumCfgs) return 0;
+  const Cfg c = kCfgs[cfg];
+  return c.nst == 3 && c.sch == 0 && R == 1 && S == 1 && stride == 1 && pad == 0 &&
+         damd_conv_supported(C, K, R, S, stride, pad, 1, cfg);
+}
+
+// pro: the input is a = relu(x * p_scale + p_shift [+ p_res]) (ProArgs), 1x1 / stride 1 only
 int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
                          int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi,
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
-                         const float* scale, const float* shift) {
+                         const float* scale, const float* shift, int pro, const void* p_res, const float* p_scale,
+                         const float* p_shift, void* p_aout, uint8_t* p_mout) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
+  if (pro && (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg) || p_scale == nullptr || p_shift == nullptr))
+    return -4;
+  const ProArgs pa{static_cast<const bf16_t*>(p_res), p_scale, p_shift, static_cast<bf16_t*>(p_aout), p_mout};
   if (epi < 0 || epi > 3 || (epi != 0 && part == nullptr)) return -3;
   if (epi >= 2 && (yb == nullptr || mean == nullptr || (epi == 2 && mask == nullptr) ||
                    (epi == 3 && (scale == nullptr || shift == nullptr))))
@@ -890,8 +996,16 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
-#define L1(BCO, BP, WCO, NW, NST, E, SC) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea)
+#define L1(BCO, BP, WCO, NW, NST, E, SC)                                                                  \
+  do {                                                                                                     \
+    if constexpr (NST == 3 && SC == 0) {                                                                   \
+      if (pro) {                                                                                           \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 1>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+        break;                                                                                             \
+      }                                                                                                    \
+    }                                                                                                      \
+    hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 0>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+  } while (0)
 #define LS(BCO, BP, WCO, NW, NST, SC)                          \
   do {                                                         \
     switch (epi) {                                             \

@@ -257,13 +257,18 @@ class _BNActConvFn(torch.autograd.Function):
     unsupported) the backward is the unfused composition."""
 
     @staticmethod
-    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg):
+    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg, pro):
         from determined_amd import ops
 
         e = ops.ext()
-        a, stats, mask = e.bn_act_fwd(y, bn_w, bn_b, rm, rv, float(momentum), float(eps), residual, True, True,
-                                      stats_part)
-        z, part = e.conv_fwd(a, conv_w, stride, pad, True, cfg, 0)
+        if pro:  # 1x1 conv applies the BN(+residual)+ReLU while staging its input (conv_igemm.hip PRO)
+            stats = e.bn_finalize_part(stats_part, y.numel() // y.shape[1], bn_w, bn_b, rm, rv, float(momentum),
+                                       float(eps))
+            z, part, a, mask = e.conv_bnact_fwd(y, conv_w, residual, stats, residual is not None, cfg)
+        else:
+            a, stats, mask = e.bn_act_fwd(y, bn_w, bn_b, rm, rv, float(momentum), float(eps), residual, True, True,
+                                          stats_part)
+            z, part = e.conv_fwd(a, conv_w, stride, pad, True, cfg, 0)
         masked = mask.numel() > 0
         ctx.save_for_backward(y, stats, bn_w, mask if masked else None, a, conv_w,
                               residual if (residual is not None and not masked) else None)
@@ -303,7 +308,7 @@ class _BNActConvFn(torch.autograd.Function):
             if g_a is not None and mask is None:
                 da, g_a = da + g_a, None
             dy, dg, db, dres = e.bn_act_bwd(da, y, residual, stats, bn_w, True, has_res, mask, g_a)
-        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None)
+        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None)
 
 
 def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tensor], residual: Optional[torch.Tensor],
@@ -321,13 +326,26 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         rm, rv, momentum = bn.train_step_args()
         st, pad = conv.stride[0], conv.padding[0]
         w = conv.weight
+        pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
+                    if stats_part is not None and ops.fusion_enabled("bn_prologue") else [])
+        if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
+            key = ("fwd_pro", tuple(y.shape), tuple(w.shape), residual is not None)
+            cfg = _TUNE.get(key)
+            if cfg is None:  # tune on stand-in BN parameters (timing does not depend on them)
+                dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
+                dummy[2].fill_(1.0)
+                cands = {c: (lambda c=c: e.conv_bnact_fwd(y, w, residual, dummy, residual is not None, c))
+                         for c in pro_cfgs}
+                cfg = _pick(key, cands, default=pro_cfgs[-1])
+            return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st,
+                                      pad, cfg, True)
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
         cfg = _TUNE.get(key)
         if cfg is None:  # tune the conv on a stand-in input of the same shape
             cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w, st, pad)}
             cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
         return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,
-                                  cfg)
+                                  cfg, False)
     a = bn(y, residual, stats_part=stats_part)
     z, part = conv_bn_input(conv, a)
     return a, z, part

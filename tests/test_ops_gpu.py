@@ -483,3 +483,49 @@ def test_chained_bottlenecks_match_unchained(ops, monkeypatch, depth):
         e_on = ((on[n] - r).norm() / r.norm()).item()
         e_off = ((off[n] - r).norm() / r.norm()).item()
         assert e_on < max(2 * e_off, 3e-2), (n, e_on, e_off)
+
+
+@pytest.mark.parametrize("with_res", [True, False])
+def test_conv_bnact_prologue_matches_composition(ops, with_res):
+    """conv_bnact_fwd: BN(+residual)+ReLU applied in the 1x1 conv's operand staging vs bn_act_fwd +
+    conv_fwd: a, its mask, z and z's statistics, for every prologue-capable config."""
+    e = ops.ext()
+    torch.manual_seed(0)
+    cl = torch.channels_last
+    n, cin, cout, hw = 3, 256, 128, 13  # M = 507: a partial last tile
+    y = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    res = torch.randn_like(y) if with_res else None
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    bnw = torch.rand(cin, device="cuda") + 0.5
+    bnb = torch.randn(cin, device="cuda") * 0.2
+    a_ref, stats, mask_ref = e.bn_act_fwd(y, bnw, bnb, None, None, 0.0, 1e-5, res, True, True, None)
+    z_ref = torch.nn.functional.conv2d(a_ref.float(), w.float())
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
+    assert cfgs
+    for cfg in cfgs:
+        z, part, a, mask = e.conv_bnact_fwd(y, w, res, stats, with_res, cfg)
+        torch.testing.assert_close(a, a_ref, rtol=0, atol=0)
+        if with_res:
+            assert torch.equal(mask, mask_ref)
+        else:
+            assert mask.numel() == 0
+        torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())
+        tol = 2e-3 * z_ref.abs().sum((0, 2, 3)).max().item()
+        torch.testing.assert_close(part[:, 0].sum(0), z_ref.sum((0, 2, 3)), rtol=1e-3, atol=tol)
+
+
+def test_bn_finalize_part_matches_bn_act_fwd(ops):
+    e = ops.ext()
+    torch.manual_seed(1)
+    y = torch.randn(4, 64, 9, 9, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    yf = y.float()
+    part = torch.stack([yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))]).unsqueeze(0).contiguous()
+    w = torch.rand(64, device="cuda") + 0.5
+    b = torch.randn(64, device="cuda")
+    rm1, rv1 = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    st = e.bn_finalize_part(part, y.numel() // 64, w, b, rm1, rv1, 0.1, 1e-5)
+    _, st_ref, _ = e.bn_act_fwd(y, w, b, rm2, rv2, 0.1, 1e-5, None, True, False, None)
+    torch.testing.assert_close(st, st_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rm1, rm2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-4, atol=1e-5)
