@@ -726,7 +726,7 @@ struct WGeo {
   FastDiv dOHW, dOW;
 };
 
-template <int BCO, int BKC, int WCO>
+template <int BCO, int BKC, int WCO, int NST = 2>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part, WGeo g) {
   constexpr int WK = 4 / WCO;
@@ -737,7 +737,9 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
   constexpr int BLK = 64 * 64;                    // elements per [64 px][64 ch] block
   constexpr int STAGE = (ACB + BCB) * BLK;
   constexpr int NI = (ACB + BCB) * 8 / 4;         // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  static_assert(NST == 2 || NST == 3, "ring depth");
+  constexpr int NLW = NI;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE];
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c16 = lane & 15, lg = lane >> 4;
@@ -810,12 +812,17 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  if (items > 0) issue(0, 0);
+#pragma unroll
+  for (int s0 = 0; s0 < NST - 1; ++s0)
+    if (s0 < items) issue(s0, s0);
   for (int it = 0; it < items; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (it + 1 < items) issue((it + 1) & 1, it + 1);
-    const bf16_t* sa = lds + (it & 1) * STAGE;
+    // retire slot it; with the 3-slot ring the next slot's DMAs stay in flight (counted wait,
+    // raw barrier: a __syncthreads() fence would drain the ring)
+    if (NST == 3 && it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NLW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + NST - 1 < items) issue((it + NST - 1) % NST, it + NST - 1);
+    const bf16_t* sa = lds + (it % NST) * STAGE;
     const bf16_t* sb = sa + ACB * BLK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -852,36 +859,46 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
       }
 }
 
-// dW = sum over splits of part[split][n], 4 consecutive outputs per thread; eight independent
-// partial sums (splits k, k+8, ...) keep eight loads in flight instead of one dependent chain,
-// combined in a fixed order (deterministic).
+// dW = sum over splits of part[split][n].  A 256-thread block owns 64 float4 columns; its 4 waves
+// each sum every 4th split with 4 independent accumulators (16 loads in flight per wave instead
+// of one dependent chain per column), then the 4 wave sums are combined in LDS in a fixed order
+// (deterministic).
 template <typename WT>
 __global__ void __launch_bounds__(256)
 wgrad_finalize_kernel(const float* __restrict__ part, int splits, int64_t n, WT* __restrict__ dw) {
-  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
-  if (i >= n) return;
-  float4 a[8];
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 64 + lane) * 4;
+  float4 a[4];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int k = 0;
-  for (; k + 8 <= splits; k += 8) {
+  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n) {
+    int k = wv;
+    for (; k + 12 < splits; k += 16) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k + u) * n + i);
-      a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k + 4 * u) * n + i);
+        a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+      }
     }
-  }
-  for (; k < splits; ++k) {  // tail (< 8 splits) into one accumulator: no runtime-indexed array
-    const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + i);
-    a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    for (; k < splits; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + i);
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
   }
   float4 s = a[0];
 #pragma unroll
-  for (int u = 1; u < 8; ++u) { s.x += a[u].x; s.y += a[u].y; s.z += a[u].z; s.w += a[u].w; }
-  Elem<WT>::st(dw, i, s.x);
-  Elem<WT>::st(dw, i + 1, s.y);
-  Elem<WT>::st(dw, i + 2, s.z);
-  Elem<WT>::st(dw, i + 3, s.w);
+  for (int u = 1; u < 4; ++u) { s.x += a[u].x; s.y += a[u].y; s.z += a[u].z; s.w += a[u].w; }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && i < n) {
+#pragma unroll
+    for (int u = 1; u < 4; ++u) { s.x += red[u][lane].x; s.y += red[u][lane].y; s.z += red[u][lane].z; s.w += red[u][lane].w; }
+    Elem<WT>::st(dw, i, s.x);
+    Elem<WT>::st(dw, i + 1, s.y);
+    Elem<WT>::st(dw, i + 2, s.z);
+    Elem<WT>::st(dw, i + 3, s.w);
+  }
 }
 
 
@@ -1069,10 +1086,12 @@ FastDiv make_fastdiv(uint32_t d) {
   return FastDiv{d, static_cast<uint32_t>(mul), l};
 }
 struct WCfg {
-  int bco, bkc, wco;
+  int bco, bkc, wco, nst;
 };
-// 0: 128x128 (2x2 waves), 1: 64x128 (1x4), 2: 128x64 (4x1), 3: 64x64 (2x2: 32x32 per wave)
-constexpr WCfg kWCfgs[] = {{128, 128, 2}, {64, 128, 1}, {128, 64, 4}, {64, 64, 2}};
+// 0: 128x128 (2x2 waves), 1: 64x128 (1x4), 2: 128x64 (4x1), 3: 64x64 (2x2: 32x32 per wave);
+// 4-7: the same tiles with a 3-slot ring
+constexpr WCfg kWCfgs[] = {{128, 128, 2, 2}, {64, 128, 1, 2}, {128, 64, 4, 2}, {64, 64, 2, 2},
+                           {128, 128, 2, 3}, {64, 128, 1, 3}, {128, 64, 4, 3}, {64, 64, 2, 3}};
 constexpr int kNumWCfgs = sizeof(kWCfgs) / sizeof(kWCfgs[0]);
 }  // namespace
 
@@ -1118,14 +1137,21 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
   const dim3 grid(static_cast<unsigned>(g.cotiles * g.ktiles * splits));
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
+#define WG(BCO, BKC, WCO, NST) \
+  hipLaunchKernelGGL((conv_wgrad_kernel<BCO, BKC, WCO, NST>), grid, dim3(kThreads), 0, st, xp, dp, part, g)
   switch (cfg) {
-    case 0: hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
-    case 1: hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
-    case 2: hipLaunchKernelGGL((conv_wgrad_kernel<128, 64, 4>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
-    default: hipLaunchKernelGGL((conv_wgrad_kernel<64, 64, 2>), grid, dim3(kThreads), 0, st, xp, dp, part, g); break;
+    case 0: WG(128, 128, 2, 2); break;
+    case 1: WG(64, 128, 1, 2); break;
+    case 2: WG(128, 64, 4, 2); break;
+    case 3: WG(64, 64, 2, 2); break;
+    case 4: WG(128, 128, 2, 3); break;
+    case 5: WG(64, 128, 1, 3); break;
+    case 6: WG(128, 64, 4, 3); break;
+    default: WG(64, 64, 2, 3); break;
   }
+#undef WG
   const int64_t n = static_cast<int64_t>(K) * R * S * C;  // multiple of 4 (C % 64 == 0)
-  const dim3 fg(static_cast<unsigned>((n / 4 + 255) / 256));
+  const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)
     hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
   else
