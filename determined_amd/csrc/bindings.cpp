@@ -69,7 +69,7 @@ extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, i
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
                                     const float*, const float*, const float*, int, const void*, const float*,
-                                    const float*, void*, uint8_t*);
+                                    const float*, const float*, void*, uint8_t*);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
@@ -77,6 +77,9 @@ void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const voi
                         float, float, float*, float*, float*, float*, float*, int, int, int, hipStream_t, uint8_t*, const float*, int);
 void damd_bn_bwd_from_part_launch(const void*, const void*, int64_t, int, const float*, const float*, const float*,
                                   const float*, int, float*, void*, void*, void*, int, int, hipStream_t);
+void damd_bn_bwd_finalize_launch(const float*, int, int, int64_t, const float*, const float*, const float*, float*, void*,
+                                 void*, int, hipStream_t);
+void damd_bn_bwd_apply_coef_launch(const void*, const void*, int64_t, int, const float*, void*, int, hipStream_t);
 void damd_bn_finalize_launch(const float*, int, int, int64_t, const void*, const void*, float*, float*, float, float,
                              float*, float*, float*, float*, int, hipStream_t);
 void damd_bn_apply_only_launch(const void*, const void*, void*, int64_t, int, const float*, const float*, int, int,
@@ -448,6 +451,36 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// BN backward finalize only: (coef [3, C] = A, B, Cc with dx = A*dz + B*x + Cc, dgamma, dbeta)
+std::vector<at::Tensor> bn_bwd_finalize_part(const at::Tensor& x, const at::Tensor& stats, const at::Tensor& weight,
+                                             const at::Tensor& part) {
+  TORCH_CHECK(bn_supported(x), "bn_bwd_finalize_part: unsupported x");
+  const int64_t C = bn_channels(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 3 && part.size(1) == 2 && part.size(2) == C &&
+              part.is_contiguous(), "bn_bwd_finalize_part: part must be float32 [nb, 2, C]");
+  auto coef = at::empty({3, C}, x.options().dtype(at::kFloat));
+  auto dgamma = at::empty({C}, weight.options());
+  auto dbeta = at::empty({C}, weight.options());
+  damd_bn_bwd_finalize_launch(part.data_ptr<float>(), static_cast<int>(part.size(0)), static_cast<int>(C), M,
+                              stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
+                              coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(), dtype_code(weight),
+                              cur_stream());
+  return {coef, dgamma, dbeta};
+}
+
+// dx = coef[0] * dz + coef[1] * x + coef[2] (the BN backward apply pass, no mask)
+at::Tensor bn_bwd_apply_coef(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& coef) {
+  check_bn_tensor(dz, x, "dz");
+  TORCH_CHECK(bn_supported(x), "bn_bwd_apply_coef: unsupported x");
+  const int64_t C = bn_channels(x);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.numel() == 3 * C && coef.is_contiguous(), "bn_bwd_apply_coef: coef");
+  auto dx = at::empty_like(x);
+  damd_bn_bwd_apply_coef_launch(dz.data_ptr(), x.data_ptr(), x.numel() / C, static_cast<int>(C), coef.data_ptr<float>(),
+                                dx.data_ptr(), dtype_code(x), cur_stream());
+  return dx;
+}
+
 // BN forward statistics (mean, invstd, scale, shift) [4, C] from producer partials [nb, 2, C]
 // of a tensor with M rows; updates the running statistics.
 at::Tensor bn_finalize_part(const at::Tensor& part, int64_t M, const at::Tensor& weight, const at::Tensor& bias,
@@ -726,7 +759,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr);
+                                      nullptr, nullptr, nullptr);
   TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
   return {y, part};
 }
@@ -760,7 +793,7 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 1,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
-                                      stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), a.data_ptr(),
+                                      stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), nullptr, a.data_ptr(),
                                       want_mask ? mask.data_ptr<uint8_t>() : nullptr);
   TORCH_CHECK(rc == 0, "conv_bnact_fwd: launch rejected");
   return {z, part, a, mask};
@@ -780,7 +813,8 @@ bool conv_pro_supported(const at::Tensor& y, const at::Tensor& w, int64_t cfg) {
 // from yb * scale + shift (no residual).  stats: [4, C] (mean, invstd, scale, shift).
 std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt, int64_t pad, int64_t cfg,
                                       const c10::optional<at::Tensor>& d2, const at::Tensor& yb,
-                                      const c10::optional<at::Tensor>& mask, const at::Tensor& stats) {
+                                      const c10::optional<at::Tensor>& mask, const at::Tensor& stats,
+                                      const c10::optional<at::Tensor>& pro_y, const c10::optional<at::Tensor>& pro_coef) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(wt.size(0)), 0);
   TORCH_CHECK(conv_supported(dy, wt, cfg, 1, pad), "conv_dgrad_bn: unsupported input / weight / config");
   const int64_t N = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
@@ -809,13 +843,40 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
   auto dz = at::empty_like(yb);
   const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
   auto part = at::empty({G, 2, K}, dy.options().dtype(at::kFloat));
+  // Deferred BN-backward apply (ops/conv.py _LazyBNGrad): with pro_y given, `dy` holds the
+  // following BatchNorm's output gradient dz and the conv's real output gradient is
+  // pro_coef[0] * dz + pro_coef[1] * pro_y + pro_coef[2] (per channel), formed in the operand
+  // staging and returned materialised as a third output for the weight gradient.
+  int pro = 0;
+  const void* p_res = nullptr;
+  const float *p_a = nullptr, *p_b = nullptr, *p_c = nullptr;
+  void* p_out = nullptr;
+  at::Tensor dyo;
+  if (pro_y.has_value() && pro_y->defined()) {
+    TORCH_CHECK(pro_coef.has_value() && pro_coef->defined() && pro_coef->scalar_type() == at::kFloat &&
+                pro_coef->dim() == 2 && pro_coef->size(0) == 3 && pro_coef->size(1) == C && pro_coef->is_contiguous(),
+                "conv_dgrad_bn: pro_coef must be float32 [3, C]");
+    TORCH_CHECK(pro_y->sizes() == dy.sizes() && pro_y->strides() == dy.strides() &&
+                pro_y->scalar_type() == at::kBFloat16, "conv_dgrad_bn: pro_y must match dy");
+    TORCH_CHECK(damd_conv_pro_supported(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
+                                        static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(cfg)),
+                "conv_dgrad_bn: config has no prologue variant");
+    pro = 2;
+    p_res = pro_y->data_ptr();
+    p_a = (*pro_coef)[0].data_ptr<float>();
+    p_b = (*pro_coef)[1].data_ptr<float>();
+    p_c = (*pro_coef)[2].data_ptr<float>();
+    dyo = at::empty_like(dy);
+    p_out = dyo.data_ptr();
+  }
   const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
                                       yb.data_ptr(), mp, stats[0].data_ptr<float>(), stats[2].data_ptr<float>(),
-                                      stats[3].data_ptr<float>(), 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+                                      stats[3].data_ptr<float>(), pro, p_res, p_a, p_c, p_b, p_out, nullptr);
   TORCH_CHECK(rc == 0, "conv_dgrad_bn: launch rejected");
+  if (pro) return {dz, part, dyo};
   return {dz, part};
 }
 
@@ -1017,6 +1078,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("bn_bwd_from_part", &bn_bwd_from_part);
   m.def("bn_finalize_part", &bn_finalize_part);
+  m.def("bn_bwd_finalize_part", &bn_bwd_finalize_part);
+  m.def("bn_bwd_apply_coef", &bn_bwd_apply_coef);
   m.def("bn_apply", &bn_apply);
   m.def("bn_pool_fwd", &bn_pool_fwd);
   m.def("resid_norm_supported", &resid_norm_supported);

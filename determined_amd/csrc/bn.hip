@@ -864,6 +864,31 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
 // BN backward when the reduce partials (sum dz, sum dz*(x - mean)) already came out of the
 // producer of dz (the conv input-gradient epilogue, conv_igemm.hip kEpiBnb*): dz is the gradient
 // at the BN output with any ReLU mask applied, so only the finalize and one apply pass remain.
+void damd_bn_bwd_finalize_launch(const float* part, int nb, int C, int64_t M, const float* mean, const float* invstd,
+                                 const float* scale, float* coef, void* dgamma, void* dbeta, int w_dtype, hipStream_t st) {
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+                       invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
+  DAMD_CHECK_LAUNCH();
+}
+
+void damd_bn_bwd_apply_coef_launch(const void* dz, const void* x, int64_t M, int C, const float* coef, void* dx,
+                                   int x_dtype, hipStream_t st) {
+  const int TPR = C / 8;
+  const int64_t V = M * C / 8;
+  const dim3 ag(apply_grid(V, TPR));
+  if (x_dtype == 1)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dz),
+                       static_cast<const bf16_t*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<bf16_t*>(dx), nullptr, V, TPR);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dz),
+                       static_cast<const float*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<float*>(dx), nullptr, V, TPR);
+  DAMD_CHECK_LAUNCH();
+}
+
 void damd_bn_bwd_from_part_launch(const void* dz, const void* x, int64_t M, int C, const float* mean,
                                   const float* invstd, const float* scale, const float* part, int nb, float* coef,
                                   void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype, hipStream_t st) {

@@ -111,12 +111,17 @@ struct EpiArgs {
 // `a` (aout) and its ReLU bit mask (mout) for the backward / the shortcut consumer.  This fuses
 // a BatchNorm(+residual)+ReLU forward apply pass into its consuming 1x1 convolution: the
 // activation is read as (y, res) once instead of (y, res) by the BN pass and `a` by the conv.
+// PRO == 2 is the backward counterpart: the operand is a BN backward's output
+// dy = A * dz + B * y + Cc (x = dz, res = y, scale = A, rscale = B, shift = Cc, no ReLU), written to
+// aout by co tile 0 for the weight gradient -- the BN backward apply pass fused into the input
+// gradient of the conv that produced y.
 struct ProArgs {
-  const bf16_t* res;     // residual added before the ReLU, or null
-  const float* scale;    // folded BN scale / shift of the input channels [C]
-  const float* shift;
-  bf16_t* aout;          // a, [M][C], or null
-  uint8_t* mout;         // ReLU bit mask of a, [M][C/8], or null
+  const bf16_t* res;     // residual added before the ReLU (PRO 1) / BN input y (PRO 2), or null
+  const float* scale;    // per input channel [C]: folded BN scale (PRO 1) / A (PRO 2)
+  const float* shift;    //                         folded BN shift (PRO 1) / Cc (PRO 2)
+  const float* rscale;   // PRO 2: B (scale of res); PRO 1: unused (res enters with weight 1)
+  bf16_t* aout;          // the operand, [M][C], or null
+  uint8_t* mout;         // PRO 1: ReLU bit mask of a, [M][C/8], or null
 };
 
 template <int BCO, int BP, int FI, int FJ, int EPI>
@@ -342,7 +347,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   // PRO: register-staged input rows of one k-step (lane: channel chunk `slot`, rows
   // 8 * (wave + NW * i) + prow), their BN parameters, and the tile / channel block they belong to
   bf16x8 py[PRO ? NIX : 1], pr[PRO ? NIX : 1];
-  float4 psc[2], psh[2];
+  float4 psc[2], psh[2], prs[2];
   int p_pt = 0, p_cb = 0;
   auto load_px = [&](int pt, int cb) {
     p_pt = pt;
@@ -359,12 +364,23 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     psc[1] = *reinterpret_cast<const float4*>(pa.scale + cofs + 4);
     psh[0] = *reinterpret_cast<const float4*>(pa.shift + cofs);
     psh[1] = *reinterpret_cast<const float4*>(pa.shift + cofs + 4);
+    if (PRO == 2) {
+      prs[0] = *reinterpret_cast<const float4*>(pa.rscale + cofs);
+      prs[1] = *reinterpret_cast<const float4*>(pa.rscale + cofs + 4);
+    }
   };
   // transform the staged rows into LDS slot `stage` (+ a / mask stores by co tile 0)
   auto store_px = [&](int stage) {
     bf16_t* sx = lds + stage * STAGE + BCO * kBK;
     const float sc[8] = {psc[0].x, psc[0].y, psc[0].z, psc[0].w, psc[1].x, psc[1].y, psc[1].z, psc[1].w};
     const float sh[8] = {psh[0].x, psh[0].y, psh[0].z, psh[0].w, psh[1].x, psh[1].y, psh[1].z, psh[1].w};
+    float rs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rs[e] = 1.f;
+    if (PRO == 2) {
+      rs[0] = prs[0].x; rs[1] = prs[0].y; rs[2] = prs[0].z; rs[3] = prs[0].w;
+      rs[4] = prs[1].x; rs[5] = prs[1].y; rs[6] = prs[1].z; rs[7] = prs[1].w;
+    }
     const bool has_res = pa.res != nullptr;
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
@@ -373,8 +389,8 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float t = bf2f(py[i].v[e]) * sc[e] + sh[e];
-        if (has_res) t += bf2f(pr[i].v[e]);
-        v[e] = fmaxf(t, 0.f);
+        if (has_res) t += (PRO == 2 ? rs[e] : 1.f) * bf2f(pr[i].v[e]);
+        v[e] = PRO == 1 ? fmaxf(t, 0.f) : t;
       }
       bf16x8 o;
       uint32_t bits = 0;
@@ -390,7 +406,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       if (ct == 0 && m < g.M) {
         const int64_t off = static_cast<int64_t>(m) * g.C + p_cb * kBK + (slot << 3);
         if (pa.aout != nullptr) *reinterpret_cast<bf16x8*>(pa.aout + off) = o;
-        if (pa.mout != nullptr) pa.mout[off >> 3] = static_cast<uint8_t>(bits);
+        if (PRO == 1 && pa.mout != nullptr) pa.mout[off >> 3] = static_cast<uint8_t>(bits);
       }
     }
   };
@@ -988,11 +1004,13 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi,
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
                          const float* scale, const float* shift, int pro, const void* p_res, const float* p_scale,
-                         const float* p_shift, void* p_aout, uint8_t* p_mout) {
+                         const float* p_shift, const float* p_rscale, void* p_aout, uint8_t* p_mout) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
-  if (pro && (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg) || p_scale == nullptr || p_shift == nullptr))
+  if (pro < 0 || pro > 2) return -4;
+  if (pro && (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg) || p_scale == nullptr || p_shift == nullptr ||
+              (pro == 2 && (p_rscale == nullptr || p_res == nullptr))))
     return -4;
-  const ProArgs pa{static_cast<const bf16_t*>(p_res), p_scale, p_shift, static_cast<bf16_t*>(p_aout), p_mout};
+  const ProArgs pa{static_cast<const bf16_t*>(p_res), p_scale, p_shift, p_rscale, static_cast<bf16_t*>(p_aout), p_mout};
   if (epi < 0 || epi > 3 || (epi != 0 && part == nullptr)) return -3;
   if (epi >= 2 && (yb == nullptr || mean == nullptr || (epi == 2 && mask == nullptr) ||
                    (epi == 3 && (scale == nullptr || shift == nullptr))))
@@ -1016,8 +1034,12 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
 #define L1(BCO, BP, WCO, NW, NST, E, SC)                                                                  \
   do {                                                                                                     \
     if constexpr (NST == 3 && SC == 0) {                                                                   \
-      if (pro) {                                                                                           \
+      if (pro == 1) {                                                                                      \
         hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 1>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+        break;                                                                                             \
+      }                                                                                                    \
+      if (pro == 2) {                                                                                      \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 2>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
         break;                                                                                             \
       }                                                                                                    \
     }                                                                                                      \

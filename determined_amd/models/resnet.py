@@ -82,21 +82,31 @@ def _chain_blocks(blocks, x, split: bool):
     next block's first conv: the backward then fuses each BN's reduce pass into that conv's
     input-gradient epilogue.  Returns the last block's output.  Blocks expose ``convs``/``bns``
     (the main path, last BN takes the residual) and ``downsample``."""
-    pending = None  # (pre-BN output, its stats partials, residual, BN) of the previous block
+    # lazy: the pre-BN tensor came out of a bn_act_conv node whose conv is 1x1 / stride 1, which
+    # can absorb this BN's backward apply pass into its input gradient (ops/conv.py _LazyBNGrad)
+    pending = None  # (pre-BN output, its stats partials, residual, BN, lazy) of the previous block
     for i, blk in enumerate(blocks):
         convs, bns = blk.convs(), blk.bns()
         if pending is None:
             xm, xs = x if isinstance(x, tuple) else (x, x)
             y, part = conv_bn_input(convs[0], xm)
+            lazy = False
         else:
-            y_prev, p_prev, res_prev, bn_prev = pending
-            xs, y, part = bn_act_conv(bn_prev, y_prev, p_prev, res_prev, convs[0])
+            y_prev, p_prev, res_prev, bn_prev, lazy_prev = pending
+            xs, y, part = bn_act_conv(bn_prev, y_prev, p_prev, res_prev, convs[0], lazy_grad=lazy_prev)
+            lazy = _pro_conv(convs[0])
         identity = xs if blk.downsample is None else _downsample(blk.downsample, xs)
         for bn, conv in zip(bns[:-1], convs[1:]):
-            _, y, part = bn_act_conv(bn, y, part, None, conv)
-        pending = (y, part, identity, bns[-1])
-    y, part, identity, bn = pending
+            _, y, part = bn_act_conv(bn, y, part, None, conv, lazy_grad=lazy)
+            lazy = _pro_conv(conv)
+        pending = (y, part, identity, bns[-1], lazy)
+    y, part, identity, bn, _ = pending
     return bn(y, identity, stats_part=part)
+
+
+def _pro_conv(conv: nn.Conv2d) -> bool:
+    """1x1 / stride-1 convs: their input gradient can absorb the following BN's backward apply."""
+    return conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0)
 
 
 class BasicBlock(nn.Module):

@@ -247,17 +247,55 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------- BN(+residual)+ReLU -> conv
+class _LazyBNGrad:
+    """A BatchNorm backward whose apply pass is deferred into the input gradient of the conv that
+    produced the BN's input (conv_igemm.hip PRO == 2).  The BN's node returns an unwritten
+    placeholder as its input gradient and parks (dz, y, coef) here under the placeholder's
+    address; the producing conv's node -- wired to it by ``models/resnet.py _chain_blocks``, the
+    only place that sets ``lazy`` -- takes the entry, forms dy = A*dz + B*y + Cc while staging
+    its dgrad operand, and gets dy materialised for its weight gradient.  A consumer that cannot
+    fuse materialises the entry with the plain apply pass, so the placeholder is never read as
+    data."""
+
+    _pending: Dict[int, "_LazyBNGrad"] = {}
+
+    def __init__(self, placeholder: torch.Tensor, dz: torch.Tensor, y: torch.Tensor, coef: torch.Tensor):
+        self.placeholder, self.dz, self.y, self.coef = placeholder, dz, y, coef
+
+    @classmethod
+    def park(cls, dz: torch.Tensor, y: torch.Tensor, coef: torch.Tensor) -> torch.Tensor:
+        ph = torch.empty_like(y)
+        cls._pending[ph.data_ptr()] = cls(ph, dz, y, coef)
+        return ph
+
+    @classmethod
+    def take(cls, g: Optional[torch.Tensor]) -> Optional["_LazyBNGrad"]:
+        if g is None:
+            return None
+        ent = cls._pending.get(g.data_ptr())
+        if ent is None or ent.placeholder.shape != g.shape or ent.placeholder.stride() != g.stride():
+            return None
+        del cls._pending[g.data_ptr()]
+        return ent
+
+    def materialise(self) -> torch.Tensor:
+        from determined_amd import ops
+
+        return ops.ext().bn_bwd_apply_coef(self.dz, self.y, self.coef)
+
+
 class _BNActConvFn(torch.autograd.Function):
     """``a = relu(bn(y) [+ residual])``, ``z = conv(a)`` (+ the BN statistic partials of z) as one
     autograd node, so the backward can fuse the BN's reduce pass into the conv's input-gradient
     epilogue (conv_igemm.hip kEpiBnb*): the gradient at the BN output -- the conv's dX plus the
     gradient ``a`` received from its other consumer (a ResNet shortcut), ReLU-masked -- is
     written once together with its (sum, sum * (y - mean)) partials, and the BN backward is left
-    with its finalize and a single apply pass.  Without the fused kernel (strided conv, config
-    unsupported) the backward is the unfused composition."""
+    with its finalize and a single apply pass.  That apply pass is itself deferred into the
+    producer conv's input gradient when ``lazy`` (:class:`_LazyBNGrad`).  Without the fused kernel
+    (strided conv, config unsupported) the backward is the unfused composition."""
 
     @staticmethod
-    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg, pro):
+    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg, pro, lazy):
         from determined_amd import ops
 
         e = ops.ext()
@@ -272,7 +310,7 @@ class _BNActConvFn(torch.autograd.Function):
         masked = mask.numel() > 0
         ctx.save_for_backward(y, stats, bn_w, mask if masked else None, a, conv_w,
                               residual if (residual is not None and not masked) else None)
-        ctx.geo = (stride, pad, residual is not None)
+        ctx.geo = (stride, pad, residual is not None, bool(lazy))
         ctx.mark_non_differentiable(part)
         # an unused `a` (BN1/BN2 outputs have no second consumer) must arrive as None, not as a
         # materialised zero tensor that the backward would read and add
@@ -285,38 +323,57 @@ class _BNActConvFn(torch.autograd.Function):
 
         e = ops.ext()
         y, stats, bn_w, mask, a, conv_w, residual = ctx.saved_tensors
-        stride, pad, has_res = ctx.geo
+        stride, pad, has_res, lazy = ctx.geo
         cl = torch.channels_last
         k = conv_w.shape[2]
         if g_z is None:  # the conv output is always consumed in the networks this node serves
             raise RuntimeError("bn_act_conv: the conv output received no gradient")
-        g_z = g_z.contiguous(memory_format=cl)
         g_a = None if g_a is None else g_a.contiguous(memory_format=cl)
-        dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
+        parked = _LazyBNGrad.take(g_z)  # g_z may be a deferred BN backward (the next BN's node)
         wt = _flip_weight(conv_w) if stride == 1 and 2 * pad == k - 1 else None
-        fused = (wt is not None and (mask is not None or not has_res)
-                 and bool(e.conv_supported(g_z, wt, -1, 1, k - 1 - pad)))
+        fused = wt is not None and (mask is not None or not has_res)
+        pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(parked.dz, wt, c)]
+                    if parked is not None and fused else [])
+        if parked is not None and not pro_cfgs:
+            g_z, parked = parked.materialise(), None
+        if parked is None:
+            g_z = g_z.contiguous(memory_format=cl)
+            fused = fused and bool(e.conv_supported(g_z, wt, -1, 1, k - 1 - pad))
         if fused:
-            cands = {c: (lambda c=c: e.conv_dgrad_bn(g_z, wt, k - 1 - pad, c, g_a, y, mask, stats))
-                     for c in _igemm_cfgs(e, g_z, wt, 1, k - 1 - pad)}
-            key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
-            dz, part = cands[_pick(key, cands, default=e.conv_default_cfg(wt.shape[0]))]()
-            dy, dg, db = e.bn_bwd_from_part(dz, y, stats, bn_w, part)
+            if parked is not None:  # BN-backward apply of the next BN inside this dgrad's staging
+                dzn, yn, coef = parked.dz, parked.y, parked.coef
+                cands = {c: (lambda c=c: e.conv_dgrad_bn(dzn, wt, k - 1 - pad, c, g_a, y, mask, stats, yn, coef))
+                         for c in pro_cfgs}
+                key = ("dgrad_bn_pro", tuple(dzn.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+                dz, part, g_z = cands[_pick(key, cands, default=pro_cfgs[-1])]()
+            else:
+                cands = {c: (lambda c=c: e.conv_dgrad_bn(g_z, wt, k - 1 - pad, c, g_a, y, mask, stats, None, None))
+                         for c in _igemm_cfgs(e, g_z, wt, 1, k - 1 - pad)}
+                key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+                dz, part = cands[_pick(key, cands, default=e.conv_default_cfg(wt.shape[0]))]()
+            if lazy:  # defer this BN's apply pass into the conv that produced y
+                coef, dg, db = e.bn_bwd_finalize_part(y, stats, bn_w, part)
+                dy = _LazyBNGrad.park(dz, y, coef)
+            else:
+                dy, dg, db = e.bn_bwd_from_part(dz, y, stats, bn_w, part)
             dres = dz if has_res else None
         else:
             da = _dgrad(g_z, a, conv_w, stride, pad).contiguous(memory_format=cl)
             if g_a is not None and mask is None:
                 da, g_a = da + g_a, None
             dy, dg, db, dres = e.bn_act_bwd(da, y, residual, stats, bn_w, True, has_res, mask, g_a)
-        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None)
+        dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
+        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None, None)
 
 
 def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tensor], residual: Optional[torch.Tensor],
-                conv: nn.Conv2d) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+                conv: nn.Conv2d, lazy_grad: bool = False) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
     """``a = bn(y, residual, stats_part=stats_part)`` (a ``BatchNormAct2d`` with ReLU) followed by
     ``z, part = conv_bn_input(conv, a)``; returns ``(a, z, part)``.  Training-mode bf16
     channels-last inputs run as one fused autograd node (:class:`_BNActConvFn`); anything else
-    is that exact composition."""
+    is that exact composition.  ``lazy_grad``: ``y`` is the ``z`` of another ``bn_act_conv``
+    node (its only consumer being this one), which may then take this BN's backward apply pass
+    into its own input gradient (:class:`_LazyBNGrad`)."""
     from determined_amd import ops
     from determined_amd.ops.bn import BatchNormAct2d
 
@@ -326,6 +383,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         rm, rv, momentum = bn.train_step_args()
         st, pad = conv.stride[0], conv.padding[0]
         w = conv.weight
+        lazy = bool(lazy_grad) and ops.fusion_enabled("bn_lazy_bwd")
         pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
                     if stats_part is not None and ops.fusion_enabled("bn_prologue") else [])
         if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
@@ -338,14 +396,14 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                          for c in pro_cfgs}
                 cfg = _pick(key, cands, default=pro_cfgs[-1])
             return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st,
-                                      pad, cfg, True)
+                                      pad, cfg, True, lazy)
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
         cfg = _TUNE.get(key)
         if cfg is None:  # tune the conv on a stand-in input of the same shape
             cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w, st, pad)}
             cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
         return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,
-                                  cfg, False)
+                                  cfg, False, lazy)
     a = bn(y, residual, stats_part=stats_part)
     z, part = conv_bn_input(conv, a)
     return a, z, part

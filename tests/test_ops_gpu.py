@@ -436,7 +436,7 @@ def test_conv_dgrad_bn_epilogue(ops, k, masked, with_d2):
     cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_supported(g, wt, c, 1, k // 2)]
     assert cfgs
     for cfg in cfgs:  # generic and (3x3) halo kernels
-        dz, part = e.conv_dgrad_bn(g, wt, k // 2, cfg, d2, yb, mask if masked else None, stats)
+        dz, part = e.conv_dgrad_bn(g, wt, k // 2, cfg, d2, yb, mask if masked else None, stats, None, None)
         torch.testing.assert_close(dz.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
         dzf = dz.float()
         torch.testing.assert_close(part[:, 0].sum(0), dzf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
@@ -475,8 +475,11 @@ def test_chained_bottlenecks_match_unchained(ops, monkeypatch, depth):
         grads["x"] = x.grad.float().cpu()
         return y.detach().float().cpu(), grads
 
+    from determined_amd.ops.conv import _LazyBNGrad
+
     yr, ref = run(torch.float32, False)
     yc, on = run(torch.bfloat16, True)
+    assert not _LazyBNGrad._pending  # every deferred BN backward was taken by its producer
     yu, off = run(torch.bfloat16, False)
     assert ((yc - yr).norm() / yr.norm()).item() < 2e-2
     for n, r in ref.items():
@@ -529,3 +532,32 @@ def test_bn_finalize_part_matches_bn_act_fwd(ops):
     torch.testing.assert_close(st, st_ref, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(rm1, rm2, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rv1, rv2, rtol=1e-4, atol=1e-5)
+
+
+def test_conv_dgrad_bn_with_deferred_bn_apply(ops):
+    """conv_dgrad_bn with pro_y/pro_coef: the operand dy = A*dz + B*y + Cc is formed in the dgrad's
+    staging (the next BN's backward apply pass) and returned materialised; dz / partials match
+    the kernel run on the explicitly applied dy."""
+    e = ops.ext()
+    torch.manual_seed(3)
+    cl = torch.channels_last
+    n, cin, cout, hw = 3, 128, 256, 11
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
+    wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)
+    dzn = torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yn = torch.randn_like(dzn)
+    coef = torch.randn(3, cout, device="cuda").contiguous()
+    yb = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    _, stats, _ = e.bn_act_fwd(yb, torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2,
+                               None, None, 0.0, 1e-5, None, True, False, None)
+    dy_ref = e.bn_bwd_apply_coef(dzn, yn, coef)
+    torch.testing.assert_close(dy_ref.float(), (coef[0].view(1, -1, 1, 1) * dzn.float() + coef[1].view(1, -1, 1, 1)
+                                                * yn.float() + coef[2].view(1, -1, 1, 1)), rtol=1e-2, atol=1e-2)
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(dzn, wt, c)]
+    assert cfgs
+    for cfg in cfgs:
+        dz_ref, part_ref = e.conv_dgrad_bn(dy_ref, wt, 0, cfg, None, yb, None, stats, None, None)
+        dz, part, dy = e.conv_dgrad_bn(dzn, wt, 0, cfg, None, yb, None, stats, yn, coef)
+        torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)  # fma order may differ by 1 ulp
+        torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(part, part_ref, rtol=1e-3, atol=1e-2)
