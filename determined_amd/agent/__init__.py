@@ -2,9 +2,10 @@
 (reference: ``agent/`` in Go, which launches Docker containers).
 
 On an MI355X node the agent owns 8 GPU slots (one per GPU, discovered from the KFD topology in
-sysfs -- the agent never initialises HIP itself, so spawning task processes is safe).  Tasks
-run as process groups with ``HIP_VISIBLE_DEVICES`` set to their slots; stdout/stderr are
-shipped to the master line by line; exit codes are reported back.
+sysfs -- the agent never initialises HIP itself, so spawning task processes is safe).  By default
+tasks run as process groups with ``HIP_VISIBLE_DEVICES`` set to their slots; an agent can
+instead front a Slurm/PBS partition or a Kubernetes namespace (``agent/backends.py``).
+stdout/stderr are shipped to the master line by line; exit codes are reported back.
 """
 
 import base64
@@ -14,15 +15,14 @@ import logging
 import os
 import pathlib
 import shlex
-import signal
 import socket
-import subprocess
 import sys
 import tarfile
 import threading
 import time
 from typing import Any, Dict, List, Optional
 
+from determined_amd.agent.backends import ProcessBackend, TaskHandle
 from determined_amd.common.api import Session
 
 logger = logging.getLogger("determined_amd.agent")
@@ -52,15 +52,16 @@ def detect_gpus() -> List[int]:
 class _Task:
     def __init__(self, cmd: Dict[str, Any]) -> None:
         self.cmd = cmd
-        self.proc: Optional[subprocess.Popen] = None
+        self.handle: Optional[TaskHandle] = None
         self.killed = False
 
 
 class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, slots: Optional[int] = None,
                  gpus: Optional[List[int]] = None, work_root: Optional[str] = None, host: Optional[str] = None,
-                 token: Optional[str] = None, label: str = "") -> None:
+                 token: Optional[str] = None, label: str = "", backend: Any = None) -> None:
         self.session = Session(master_url, token=token)
+        self.backend = backend or ProcessBackend()
         self.agent_id = agent_id or socket.gethostname()
         self.gpus = detect_gpus() if gpus is None else gpus
         self.use_gpu = bool(self.gpus) and slots is None
@@ -140,22 +141,26 @@ class Agent:
         code = -1
         try:
             wd = self._prepare_workdir(c)
-            env = dict(os.environ)
-            env.update({k: str(v) for k, v in c.get("env", {}).items()})
+            # the task's own variables; a process backend layers them over the agent's environment,
+            # batch / pod backends ship only these
+            env = {k: str(v) for k, v in c.get("env", {}).items()}
             env["DET_MODEL_DEF_DIR"] = str(wd)
-            env["PYTHONPATH"] = os.pathsep.join([str(wd), _repo_root()] + [p for p in [env.get("PYTHONPATH")] if p])
-            env["HSA_ENABLE_IPC_MODE_LEGACY"] = env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            env["PYTHONPATH"] = os.pathsep.join([str(wd), _repo_root()] +
+                                                [p for p in [os.environ.get("PYTHONPATH")] if p])
+            env["HSA_ENABLE_IPC_MODE_LEGACY"] = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             devices = c.get("devices", [])
             if c.get("gpu"):
-                env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+                if self.backend.sets_visible_devices:
+                    env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
             else:
                 env["DET_CPU_SLOTS"] = str(len(devices))
             argv = self._command(c)
             self.session.post(f"/api/v1/agents/{self.agent_id}/events", {"type": "started", "allocation_id": aid})
-            t.proc = subprocess.Popen(argv, cwd=wd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                      start_new_session=True, text=True, bufsize=1)
+            t.handle = self.backend.launch(argv, wd, env, c)
+            if t.killed:  # a kill raced the launch
+                t.handle.kill()
             self._pump_logs(t, c["task_id"], aid)
-            code = t.proc.wait()
+            code = t.handle.wait()
         except Exception as e:
             logger.exception(f"task {aid} failed to run")
             self._ship(c["task_id"], aid, [f"agent: task failed to start: {e!r}"])
@@ -168,16 +173,34 @@ class Agent:
                 logger.warning(f"could not report exit of {aid}: {e}")
 
     def _pump_logs(self, t: _Task, task_id: str, aid: str) -> None:
-        assert t.proc is not None and t.proc.stdout is not None
+        """Ship log lines in batches (<= 200 lines or 0.5 s old); a flusher thread sends a partial
+        batch when the task goes quiet, so the last line before a long silence is not held back."""
+        assert t.handle is not None
         buf: List[str] = []
-        last = time.time()
-        for line in t.proc.stdout:
-            buf.append(line.rstrip("\n"))
-            if len(buf) >= 200 or time.time() - last > 0.5:
-                self._ship(task_id, aid, buf)
-                buf, last = [], time.time()
-        if buf:
-            self._ship(task_id, aid, buf)
+        lock = threading.Lock()
+        done = threading.Event()
+
+        def flush() -> None:
+            with lock:  # held while shipping: batches reach the master in order
+                if buf:
+                    self._ship(task_id, aid, buf[:])
+                    buf.clear()
+
+        def flusher() -> None:
+            while not done.wait(0.5):
+                flush()
+
+        threading.Thread(target=flusher, daemon=True).start()
+        try:
+            for line in t.handle.lines():
+                with lock:
+                    buf.append(line)
+                    full = len(buf) >= 200
+                if full:
+                    flush()
+        finally:
+            done.set()
+            flush()
 
     def _ship(self, task_id: str, aid: str, lines: List[str]) -> None:
         logs = []
@@ -196,23 +219,11 @@ class Agent:
 
     def _kill(self, aid: str, grace: float = 10.0) -> None:
         t = self.tasks.get(aid)
-        if t is None or t.proc is None:
+        if t is None:
             return
         t.killed = True
-        try:
-            os.killpg(t.proc.pid, signal.SIGTERM)
-        except ProcessLookupError:
-            return
-
-        def hard() -> None:
-            time.sleep(grace)
-            if t.proc is not None and t.proc.poll() is None:
-                try:
-                    os.killpg(t.proc.pid, signal.SIGKILL)
-                except ProcessLookupError:
-                    pass
-
-        threading.Thread(target=hard, daemon=True).start()
+        if t.handle is not None:
+            t.handle.kill(grace)
 
 
 def _repo_root() -> str:

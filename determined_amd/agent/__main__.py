@@ -3,9 +3,11 @@
 import argparse
 import logging
 import os
+import shlex
 import sys
 
 from determined_amd.agent import Agent
+from determined_amd.agent.backends import make_backend
 
 
 def main(argv=None) -> int:
@@ -17,11 +19,35 @@ def main(argv=None) -> int:
     p.add_argument("--work-root", default=None)
     p.add_argument("--host", default=None, help="address other agents/ranks use to reach this node")
     p.add_argument("--label", default="")
+    p.add_argument("--backend", default="process", choices=["process", "slurm", "pbs", "kubernetes"],
+                   help="where tasks run: local process groups, Slurm/PBS batch jobs, or Kubernetes pods")
+    p.add_argument("--gpu-slots", type=int, default=None,
+                   help="GPU capacity this agent advertises (batch partitions / Kubernetes: the whole pool)")
+    p.add_argument("--slots-per-node", type=int, default=8, help="GPUs per batch node / per pod")
+    p.add_argument("--partition", default=None, help="Slurm partition (PBS: queue)")
+    p.add_argument("--batch-args", default="", help="extra sbatch/qsub arguments (shell-quoted string)")
+    p.add_argument("--k8s-api", default=None, help="Kubernetes API URL (default: in-cluster config)")
+    p.add_argument("--k8s-namespace", default="default")
+    p.add_argument("--k8s-image", default="determined-amd:latest")
+    p.add_argument("--k8s-token-file", default=None)
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     gpus = [int(x) for x in a.gpus.split(",")] if a.gpus else None
+    if a.gpu_slots is not None:
+        gpus = list(range(a.gpu_slots))
+    backend = None
+    if a.backend in ("slurm", "pbs"):
+        kw = {"slots_per_node": a.slots_per_node, "extra_args": shlex.split(a.batch_args)}
+        kw["partition" if a.backend == "slurm" else "queue_name"] = a.partition
+        backend = make_backend(a.backend, **kw)
+    elif a.backend == "kubernetes":
+        token = open(a.k8s_token_file).read().strip() if a.k8s_token_file else None
+        backend = make_backend("kubernetes", api_url=a.k8s_api, token=token, namespace=a.k8s_namespace,
+                               image=a.k8s_image, slots_per_pod=a.slots_per_node)
+    if backend is not None and a.slots is None and gpus is None:
+        p.error(f"--backend {a.backend} fronts a whole partition: give its GPU capacity with --gpu-slots N")
     agent = Agent(a.master_url, a.agent_id, a.slots, gpus, a.work_root, a.host,
-                  token=os.environ.get("DET_MASTER_TOKEN"), label=a.label)
+                  token=os.environ.get("DET_MASTER_TOKEN"), label=a.label, backend=backend)
     try:
         agent.run()
     except KeyboardInterrupt:

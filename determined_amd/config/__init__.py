@@ -129,6 +129,9 @@ TOP_DEFAULTS: Dict[str, Any] = {
     "scheduling_unit": 100,
     "searcher": None,
     "workspace": "",
+    # batch-scheduler knobs read by the Slurm / PBS agent backends (agent/backends.py)
+    "slurm": {"slots_per_node": None, "gpu_type": None, "sbatch_args": None},
+    "pbs": {"slots_per_node": None, "pbsbatch_args": None},
 }
 
 HP_TYPES = ("const", "int", "double", "log", "categorical")
@@ -296,6 +299,20 @@ def validate(cfg: Dict[str, Any]) -> List[str]:
         errs.append("optimizations.aggregation_frequency: must be >= 1")
     if not isinstance(cfg.get("scheduling_unit", 100), int) or cfg.get("scheduling_unit", 100) < 1:
         errs.append("scheduling_unit: must be >= 1")
+    for sec, args_key, allowed in (("slurm", "sbatch_args", {"slots_per_node", "gpu_type", "sbatch_args"}),
+                                   ("pbs", "pbsbatch_args", {"slots_per_node", "pbsbatch_args"})):
+        hpc = cfg.get(sec) or {}
+        if not isinstance(hpc, dict):
+            errs.append(f"{sec}: must be a mapping")
+            continue
+        for k in sorted(set(hpc) - allowed):
+            errs.append(f"{sec}.{k}: unknown field (one of {sorted(allowed)})")
+        spn = hpc.get("slots_per_node")
+        if spn is not None and (not isinstance(spn, int) or spn < 1):
+            errs.append(f"{sec}.slots_per_node: must be a positive integer")
+        extra = hpc.get(args_key)
+        if extra is not None and (not isinstance(extra, list) or not all(isinstance(x, str) for x in extra)):
+            errs.append(f"{sec}.{args_key}: must be a list of strings")
     return errs
 
 

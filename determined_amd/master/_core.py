@@ -42,6 +42,10 @@ class Allocation:
         self.killed = False
         self.exit_codes: Dict[str, int] = {}
         self.start_time = time.time()
+        # current all-gather round: request_uuid -> (order key, data); result once complete
+        self.gather: Dict[str, Tuple[Any, Any]] = {}
+        self.gather_result: Optional[List[Any]] = None
+        self.gather_fetched: set = set()
 
     def to_dict(self) -> Dict[str, Any]:
         return {"allocation_id": self.id, "task_id": self.task_id, "slots": self.slots, "state": self.state,
@@ -857,6 +861,37 @@ class Master:
             while not a.preempt and time.time() < deadline and not self._closed:
                 self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
             return a.preempt
+
+    def allocation_all_gather(self, alloc_id: str, request_uuid: str, num_peers: int, data: Any,
+                              rank: Optional[int] = None, timeout: float = 600.0) -> List[Any]:
+        """Block until ``num_peers`` processes of the allocation have posted, then return every
+        peer's ``data`` (ordered by ``rank`` when given, else by arrival).  Containers use it to
+        exchange addresses when the launcher cannot know them up front (Kubernetes pods);
+        reference ``master/internal/task/allgather``."""
+        deadline = time.time() + timeout
+        with self.lock:
+            a = self.allocations.get(alloc_id)
+            if a is None:
+                raise KeyError(f"allocation {alloc_id} not found")
+            if a.gather_result is not None and (request_uuid in a.gather_fetched
+                                                or len(a.gather_fetched) >= len(a.gather_result)):
+                a.gather_result, a.gather_fetched = None, set()  # a peer starting the next round
+            if a.gather_result is None:
+                a.gather[request_uuid] = (rank if rank is not None else len(a.gather), data)
+                if len(a.gather) >= num_peers:
+                    a.gather_result = [d for _, d in sorted(a.gather.values(), key=lambda kv: kv[0])]
+                    a.gather = {}
+                    self.cv.notify_all()
+            while a.gather_result is None and time.time() < deadline and not self._closed:
+                if a.state == "TERMINATED":
+                    raise RuntimeError(f"allocation {alloc_id} terminated during all-gather")
+                self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
+            if a.gather_result is None:
+                a.gather.pop(request_uuid, None)
+                raise TimeoutError(f"all-gather of allocation {alloc_id} timed out")
+            out = list(a.gather_result)
+            a.gather_fetched.add(request_uuid)
+            return out
 
     def ack_preemption(self, alloc_id: str) -> None:
         with self.lock:

@@ -334,6 +334,11 @@ def build_routes(m: Master) -> List[Route]:
         m.ack_preemption(aid)
         return {}
 
+    @route("POST", r"/api/v1/allocations/([^/]+)/all_gather")
+    def all_gather(q, b, aid):
+        return {"data": m.allocation_all_gather(aid, str(b["request_uuid"]), int(b["num_peers"]), b.get("data"),
+                                                b.get("rank"), float(b.get("timeout_seconds", 600)))}
+
     @route("GET", "/api/v1/allocations")
     def allocs(q, b):
         return {"allocations": [a.to_dict() for a in m.allocations.values() if a.state != "TERMINATED"]}

@@ -68,10 +68,11 @@ def test_linear_gelu_fallback_matches_composition():
 def test_disable_fusions_env_switch():
     code = ("import determined_amd.ops as o; "
             "print(o.fusion_enabled('split_grad'), o.fusion_enabled('stem_conv'), o.fusion_enabled('avgpool'), "
-            "o.fusion_enabled('igemm_conv'), o.fusion_enabled('conv_stats'))")
-    env = dict(os.environ, PYTHONPATH=ROOT, DAMD_DISABLE_FUSIONS="split_grad, stem_conv,igemm_conv")
+            "o.fusion_enabled('igemm_conv'), o.fusion_enabled('conv_stats'), o.fusion_enabled('bn_conv'), "
+            "o.fusion_enabled('bn_prologue'), o.fusion_enabled('bn_lazy_bwd'))")
+    env = dict(os.environ, PYTHONPATH=ROOT, DAMD_DISABLE_FUSIONS="split_grad, stem_conv,igemm_conv,bn_prologue")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
-    assert out.stdout.split() == ["False", "False", "True", "False", "True"]
+    assert out.stdout.split() == ["False", "False", "True", "False", "True", "True", "False", "True"]
 
 
 def test_igemm_conv_path_falls_back_on_cpu():
