@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <mutex>
 #include <vector>
 
 namespace damd {
@@ -69,8 +70,11 @@ extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, i
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
                                     const float*, const float*, const float*, int, const void*, const float*,
-                                    const float*, const float*, void*, uint8_t*);
+                                    const float*, const float*, void*, uint8_t*, float*, int*);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
+extern "C" int64_t damd_conv_sk_ws_floats(int, int, int);
+extern "C" int damd_conv_sk_flag_words();
+extern "C" int damd_conv_cfg_is_sk(int);
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
@@ -727,6 +731,41 @@ at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::
 }
 
 // ---------------------------------------------------------------- implicit-GEMM convolution
+// Stream-K configs (conv_igemm.hip make_plan) hand partial tiles between blocks: a per-call fp32
+// slab workspace from the caching allocator (stream-ordered reuse) and a per-device buffer of flag
+// words that the kernels leave zeroed (+ a poll time-out counter at its end).  The convolutions
+// of one device run on one stream at a time, so the flag buffer is not shared between live launches.
+struct SkWorkspace {
+  at::Tensor ws;
+  float* wsp = nullptr;
+  int* flags = nullptr;
+};
+
+at::Tensor& sk_flag_buffer(const at::Device& dev) {
+  static std::mutex mu;
+  static std::map<int, at::Tensor> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  at::Tensor& t = bufs[dev.index()];
+  if (!t.defined()) t = at::zeros({damd_conv_sk_flag_words()}, at::TensorOptions().device(dev).dtype(at::kInt));
+  return t;
+}
+
+SkWorkspace sk_workspace(const at::Tensor& like, int64_t K, int64_t W, int64_t cfg) {
+  SkWorkspace s;
+  const int64_t n = damd_conv_sk_ws_floats(static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg));
+  if (n == 0) return s;
+  s.ws = at::empty({n}, like.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  s.wsp = s.ws.data_ptr<float>();
+  s.flags = sk_flag_buffer(like.device()).data_ptr<int>();
+  return s;
+}
+
+// poll time-outs recorded by stream-K launches on this device (0 unless a hand-off never arrived)
+int64_t conv_sk_timeouts(const at::Tensor& like) {
+  at::Tensor& t = sk_flag_buffer(like.device());
+  return t.narrow(0, damd_conv_sk_flag_words() - 16, 1).item<int>();
+}
+
 // x: [N, C, H, W] bf16 channels-last; w: [K, C, R, S] bf16 (made channels-last = [K][R][S][C]);
 // returns (y [N, K, OH, OW] channels-last, stats partials [groups, 2, K] or an empty tensor).
 bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg, int64_t stride, int64_t pad) {
@@ -754,12 +793,13 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg),
                                  static_cast<int>(groups));
   at::Tensor part = want_stats ? at::empty({G, 2, K}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
+  const SkWorkspace sk = sk_workspace(x, K, W, cfg);
   const int rc = damd_conv_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr, nullptr);
+                                      nullptr, nullptr, nullptr, sk.wsp, sk.flags);
   TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
   return {y, part};
 }
@@ -789,12 +829,13 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
   auto mask = want_mask ? at::empty({M * C / 8}, y.options().dtype(at::kByte)) : at::empty({0}, y.options().dtype(at::kByte));
   const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
   auto part = at::empty({G, 2, K}, y.options().dtype(at::kFloat));
+  const SkWorkspace sk = sk_workspace(y, K, W, cfg);
   const int rc = damd_conv_fwd_launch(y.data_ptr(), wl.data_ptr(), z.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 1,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
                                       stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), nullptr, a.data_ptr(),
-                                      want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+                                      want_mask ? mask.data_ptr<uint8_t>() : nullptr, sk.wsp, sk.flags);
   TORCH_CHECK(rc == 0, "conv_bnact_fwd: launch rejected");
   return {z, part, a, mask};
 }
@@ -869,12 +910,14 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
     dyo = at::empty_like(dy);
     p_out = dyo.data_ptr();
   }
+  const SkWorkspace sk = sk_workspace(dy, K, W, cfg);
   const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
                                       yb.data_ptr(), mp, stats[0].data_ptr<float>(), stats[2].data_ptr<float>(),
-                                      stats[3].data_ptr<float>(), pro, p_res, p_a, p_c, p_b, p_out, nullptr);
+                                      stats[3].data_ptr<float>(), pro, p_res, p_a, p_c, p_b, p_out, nullptr, sk.wsp,
+                                      sk.flags);
   TORCH_CHECK(rc == 0, "conv_dgrad_bn: launch rejected");
   if (pro) return {dz, part, dyo};
   return {dz, part};
@@ -1093,6 +1136,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_bnact_fwd", &conv_bnact_fwd);
   m.def("conv_pro_supported", &conv_pro_supported);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
+  m.def("conv_sk_timeouts", &conv_sk_timeouts);
+  m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
   m.def("wgrad_supported", &wgrad_supported);
   m.def("conv_wgrad", &conv_wgrad);

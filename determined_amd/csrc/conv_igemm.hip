@@ -259,13 +259,156 @@ __device__ __forceinline__ void epi_flush_sums(float (&st_s)[FI / 2][8], float (
 }
 
 
+// ============================================================================ stream-K work plans
+// A persistent launch that deals whole pixel tiles round-robin ends on a partial round: with T
+// tiles per co tile and G blocks, the slowest block computes ceil(T / G) tiles while the average is
+// T / G (ResNet-50 at batch 512: 3.06 -> 4 rounds on the 14x14 layers, 1.53 -> 2 on 7x7).  With
+// stream-K (Geo::sk) each XCD slice of the grid (G / 8 blocks, the XCD-grouped block order above)
+// takes 1/8 of the pixel tiles and cuts its (tile, k-unit) stream into equal contiguous ranges, one
+// per block, so a tile may be computed in segments by consecutive blocks.  A block's range is at
+// most: a TAIL (the end of a tile begun by earlier blocks), whole tiles, and a HEAD (the start of a
+// tile the next block finishes); it runs them as whole tiles -> HEAD -> TAIL.  A HEAD (or a MIDDLE
+// segment) is published as an fp32 slab; the block owning a tile's last unit gathers the earlier
+// segments' slabs into its accumulators and runs the epilogue (BN statistics etc. exactly once per
+// tile).  Hand-off (MI355X agent-scope protocol): slabs are stored write-through (sc1 buffer
+// stores), every storing wave drains (vmcnt(0)), a barrier, then one lane sets the block's flag with
+// a relaxed agent-scope atomic store; the consumer's lane 0 polls relaxed, takes ONE agent acquire,
+// resets the flag for the next launch, and after a barrier every wave reads the slabs with plain
+// loads.  Every block publishes before it waits, and only waits on earlier blocks of its own XCD
+// slice (dispatched before it), so the chain always drains; the poll is bounded anyway (sk.err).
+struct SkArgs {
+  float* ws;   // [nblk][BCO * BP] fp32 slabs, slot = the block's remapped id
+  int* flags;  // [nblk] 0 / 1, zero between launches (the consumer resets them)
+  int* err;    // poll time-outs (must stay 0)
+};
+
+struct Plan {
+  int nfull, t0, ts;   // whole tiles t0 + i * ts
+  int th, kh;          // HEAD: tile th, units [0, kh)
+  int tt, ka, ke;      // TAIL: tile tt, units [ka, ke)
+  int gpx, xs, j, p0;  // stream-K: blocks per XCD slice, slice, index in it, its first tile
+  int64_t U;           // units in the slice
+};
+
+__device__ __forceinline__ Plan make_plan(int grp, int groups, int ptiles, int units, int sk) {
+  Plan p{};
+  p.ts = 1;
+  if (!sk) {
+    p.nfull = grp < ptiles ? (ptiles - grp + groups - 1) / groups : 0;
+    p.t0 = grp;
+    p.ts = groups;
+    return p;
+  }
+  p.gpx = groups >> 3;
+  p.xs = grp / p.gpx;
+  p.j = grp - p.xs * p.gpx;
+  p.p0 = static_cast<int>(static_cast<int64_t>(p.xs) * ptiles / 8);
+  const int p1 = static_cast<int>(static_cast<int64_t>(p.xs + 1) * ptiles / 8);
+  p.U = static_cast<int64_t>(p1 - p.p0) * units;
+  const int64_t u0 = p.j * p.U / p.gpx, u1 = (p.j + 1) * p.U / p.gpx;
+  if (u0 >= u1) return p;
+  const int a = p.p0 + static_cast<int>(u0 / units), ka = static_cast<int>(u0 % units);
+  const int b = p.p0 + static_cast<int>(u1 / units), kb = static_cast<int>(u1 % units);
+  if (a == b) {  // the whole range lies in one tile
+    if (ka == 0) { p.th = a; p.kh = kb; } else { p.tt = a; p.ka = ka; p.ke = kb; }
+    return p;
+  }
+  int fs = a;
+  if (ka > 0) { p.tt = a; p.ka = ka; p.ke = units; fs = a + 1; }
+  p.t0 = fs;
+  p.nfull = b - fs;
+  if (kb > 0) { p.th = b; p.kh = kb; }
+  return p;
+}
+
+// Segment cursor over a plan: run 0 = whole tiles, 1 = HEAD, 2 = TAIL, 3 = done.
+struct Cursor {
+  int run, i, pt, k, kend;
+};
+
+__device__ __forceinline__ void seg_enter(Cursor& c, const Plan& p, int units) {
+  if (c.run == 0) {
+    if (c.i < p.nfull) { c.pt = p.t0 + c.i * p.ts; c.k = 0; c.kend = units; return; }
+    c.run = 1;
+  }
+  if (c.run == 1) {
+    if (p.kh > 0) { c.pt = p.th; c.k = 0; c.kend = p.kh; return; }
+    c.run = 2;
+  }
+  if (c.run == 2) {
+    if (p.ke > p.ka) { c.pt = p.tt; c.k = p.ka; c.kend = p.ke; return; }
+    c.run = 3;
+  }
+}
+
+__device__ __forceinline__ void seg_next(Cursor& c, const Plan& p, int units) {
+  if (c.run == 0) ++c.i; else ++c.run;
+  seg_enter(c, p, units);
+}
+
+__device__ __forceinline__ int plan_units(const Plan& p, int units) { return p.nfull * units + p.kh + (p.ke - p.ka); }
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// publish this block's partial tile (slot `rid`) and set its flag
+template <int FI, int FJ, int NT>
+__device__ __forceinline__ void sk_publish(const f4 (&acc)[FI][FJ], const SkArgs& sk, int rid) {
+  float* base = sk.ws + static_cast<int64_t>(rid) * (FI * FJ * 4 * NT);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, FI * FJ * 16 * NT, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)  // write-through (sc1): visible without a release fence
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, acc[i][j]), rs,
+                                             ((i * FJ + j) * NT + static_cast<int>(threadIdx.x)) * 16, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(sk.flags + rid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// add the slabs of every earlier block of this XCD slice that computed part of tile `pt`
+template <int FI, int FJ, int NT>
+__device__ __forceinline__ void sk_gather(f4 (&acc)[FI][FJ], const SkArgs& sk, const Plan& p, int pt, int units,
+                                          int ctiles, int ct) {
+  const int64_t t0u = static_cast<int64_t>(pt - p.p0) * units;  // the tile's first unit in the slice
+  if (threadIdx.x == 0) {
+    for (int jj = p.j - 1; jj >= 0; --jj) {
+      const int64_t r0 = jj * p.U / p.gpx, r1 = (jj + 1) * p.U / p.gpx;
+      if (r1 <= t0u) break;
+      if (r0 >= r1) continue;
+      int* f = sk.flags + (p.xs * p.gpx + jj) * ctiles + ct;
+      unsigned spins = 0;
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 20)) { atomicAdd(sk.err, 1); break; }
+      }
+      __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int jj = p.j - 1; jj >= 0; --jj) {
+    const int64_t r0 = jj * p.U / p.gpx, r1 = (jj + 1) * p.U / p.gpx;
+    if (r1 <= t0u) break;
+    if (r0 >= r1) continue;
+    const f4* slab = reinterpret_cast<const f4*>(sk.ws + static_cast<int64_t>((p.xs * p.gpx + jj) * ctiles + ct) *
+                                                            (FI * FJ * 4 * NT));
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) acc[i][j] += slab[(i * FJ + j) * NT + threadIdx.x];
+  }
+}
+
+
 // SCH (k-step schedule): 0 = per 32-deep half: fragment reads then its MFMAs; 1 = all fragment
 // reads of the k-step issued first (the second half's reads overlap the first half's MFMAs);
 // 2 = as 1 with s_setprio(1) over the MFMA block.
-template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0, int PRO = 0>
+template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0, int PRO = 0, int SK = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-                float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
+                float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa, SkArgs sk) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -294,8 +437,8 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
   const int ct = rid % g.ctiles, grp = rid / g.ctiles;
-  const int ntiles = grp < g.ptiles ? (g.ptiles - grp + g.groups - 1) / g.groups : 0;
-  const int items = ntiles * g.ksteps;
+  const Plan plan = make_plan(grp, g.groups, g.ptiles, g.ksteps, SK);
+  const int items = plan_units(plan, g.ksteps);
   const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
   if (EPI >= kEpiBnbM) {  // visible to every wave after the main loop's first barrier
     for (int t = threadIdx.x; t < BCO; t += NT) {
@@ -411,15 +554,27 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
   };
 
-  // load-side counters: tile, channel block, tap (r, s), k-step
-  int l_tile = 0, l_cb = 0, l_r = 0, l_s = 0, l_ks = 0;
+  // load side: segment cursor (tile, k-step range) + the k-step's channel block and tap (r, s)
+  Cursor lc{0, 0, 0, 0, 0};
+  seg_enter(lc, plan, g.ksteps);
+  int l_cb = 0, l_r = 0, l_s = 0;
+  bool l_new = true;
+  auto seed = [&]() {  // k-step lc.k = (r * S + s) * cblk + cb
+    l_cb = lc.k % g.cblk;
+    const int rs = lc.k / g.cblk;
+    l_s = rs % g.S;
+    l_r = rs / g.S;
+    l_new = true;
+  };
+  seed();
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
   auto issue = [&](int stage) {
     bf16_t* sw = lds + stage * STAGE;
-    const int pt = grp + l_tile * g.groups;
-    if (!PRO && l_ks == 0) tile_rows(pt);
+    const int pt = lc.pt;
+    if (!PRO && l_new) tile_rows(pt);
+    l_new = false;
 #pragma unroll
-    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + l_ks * kBK, sw + 8 * (wave + NW * i) * kBK);
+    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + lc.k * kBK, sw + 8 * (wave + NW * i) * kBK);
     if (!PRO) {
       const int tap = l_r * g.S + l_s;
       const int64_t soff = static_cast<int64_t>(l_r * g.W + l_s) * g.C + l_cb * kBK;  // wave-uniform
@@ -431,7 +586,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     } else {
       load_px(pt, l_cb);
     }
-    // advance (cb fastest, then s, then r, then tile)
+    // advance (cb fastest, then s, then r, then the next segment)
     if (++l_cb == g.cblk) {
       l_cb = 0;
       if (++l_s == g.S) {
@@ -439,7 +594,10 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         if (++l_r == g.R) l_r = 0;
       }
     }
-    if (++l_ks == g.ksteps) { l_ks = 0; ++l_tile; }
+    if (++lc.k == lc.kend) {
+      seg_next(lc, plan, g.ksteps);
+      seed();
+    }
   };
 
   // per-lane LDS fragment offsets (elements) for the two 32-deep k halves of a stage
@@ -486,7 +644,8 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     for (int s0 = 0; s0 < NST - 1; ++s0)
       if (s0 < items) issue(s0);
   }
-  int c_ks = 0, c_tile = 0;
+  Cursor cc{0, 0, 0, 0, 0};
+  seg_enter(cc, plan, g.ksteps);
   for (int it = 0; it < items; ++it) {
     if (PRO) {
       // weights of item it, input registers of item it+1 and this wave's LDS writes of item it
@@ -535,15 +694,19 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
           for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
       if (SCH == 2) __builtin_amdgcn_s_setprio(0);
     }
-    if (++c_ks == g.ksteps) {
-      epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, grp + static_cast<int64_t>(c_tile) * g.groups, ct, wco0, wp0, lg, rho,
-                                           g, ea, prm, y, st_s, st_q);
+    if (++cc.k == cc.kend) {
+      const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
+      if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
+        sk_publish<FI, FJ, NT>(acc, sk, rid);
+      } else {
+        if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.ksteps, g.ctiles, ct);
+        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, cc.pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+      }
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-      c_ks = 0;
-      ++c_tile;
+      seg_next(cc, plan, g.ksteps);
     }
   }
 
@@ -565,10 +728,10 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 // rows starting at ANY row (the taps shift the fragment rows by r*W + s).
 constexpr int kHaloMaxLds = 160 * 1024;
 
-template <int BCO, int BP, int WCO, int NW, int EPI>
+template <int BCO, int BP, int WCO, int NW, int EPI, int SK = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-               float* __restrict__ part, Geo g, EpiArgs ea, int HR) {
+               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -590,8 +753,9 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
   const int ct = rid % g.ctiles, grp = rid / g.ctiles;
-  const int ntiles = grp < g.ptiles ? (g.ptiles - grp + g.groups - 1) / g.groups : 0;
-  const int items = ntiles * g.ksteps;  // ksteps = 9 * cblk, tap fastest
+  // work units are 64-channel blocks (9 taps each: the halo is staged once per unit)
+  const Plan plan = make_plan(grp, g.groups, g.ptiles, g.cblk, SK);
+  const int items = 9 * plan_units(plan, g.cblk);  // tap fastest
   const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
   if (EPI >= kEpiBnbM) {
     for (int t = threadIdx.x; t < BCO; t += NT) {
@@ -610,11 +774,14 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   }
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
 
-  // load side: (tile, channel block, tap) counters, running halo count (slot parity)
-  int l_tile = 0, l_cb = 0, l_tap = 0, l_halo = 0;
+  // load side: segment cursor (tile, channel-block range), tap, running halo count (slot parity)
+  Cursor lc{0, 0, 0, 0, 0};
+  seg_enter(lc, plan, g.cblk);
+  int l_tap = 0, l_halo = 0;
   auto issue = [&](int wslot) {
+    const int l_cb = lc.k;
     if (l_tap == 0) {  // stage this tile's halo for channel block l_cb
-      const int64_t f0 = static_cast<int64_t>(grp + l_tile * g.groups) * BP - g.W - 1;
+      const int64_t f0 = static_cast<int64_t>(lc.pt) * BP - g.W - 1;
       bf16_t* hs = halo + (l_halo & 1) * HSLOT;
       for (int k0 = 8 * wave; k0 < HR; k0 += 8 * NW) {
         const int k = k0 + prow;
@@ -630,7 +797,7 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + koff, ws + 8 * (wave + NW * i) * kBK);
     if (++l_tap == 9) {
       l_tap = 0;
-      if (++l_cb == g.cblk) { l_cb = 0; ++l_tile; }
+      if (++lc.k == lc.kend) seg_next(lc, plan, g.cblk);
     }
   };
 
@@ -650,15 +817,19 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
 
   if (items > 0) issue(0);
   if (items > 1) issue(1);
-  int c_tap = 0, c_cb = 0, c_tile = 0, c_halo = 0;
+  Cursor cc{0, 0, 0, 0, 0};
+  seg_enter(cc, plan, g.cblk);
+  int c_tap = 0, c_halo = 0;
+  bool c_first = true;  // first item of a segment: per-pixel tap masks of its tile
   for (int it = 0; it < items; ++it) {
     // the next item's DMAs may stay in flight (a halo issued with it is over-waited: correct)
     if (it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (it + 2 < items) issue((it + 2) % 3);
-    const int64_t pt = grp + static_cast<int64_t>(c_tile) * g.groups;
-    if (c_tap == 0 && c_cb == 0) {
+    const int64_t pt = cc.pt;
+    if (c_first) {
+      c_first = false;
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
         const int64_t m = pt * BP + wp0 + 16 * j + rho;
@@ -705,14 +876,20 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     if (++c_tap == 9) {
       c_tap = 0;
       ++c_halo;
-      if (++c_cb == g.cblk) {
-        c_cb = 0;
-        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+      if (++cc.k == cc.kend) {
+        const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.cblk);
+        if (!whole) {
+          sk_publish<FI, FJ, NT>(acc, sk, rid);
+        } else {
+          if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.cblk, g.ctiles, ct);
+          epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+        }
 #pragma unroll
         for (int i = 0; i < FI; ++i)
 #pragma unroll
           for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        ++c_tile;
+        seg_next(cc, plan, g.cblk);
+        c_first = true;
       }
     }
   }
@@ -927,7 +1104,7 @@ using namespace damd::igemm;
 namespace {
 
 struct Cfg {
-  int bco, bp, wco, nw, nst, sch;
+  int bco, bp, wco, nw, nst, sch, sk = 0;
 };
 // 0-2: 4 waves, 2-slot ring; 3-5: 8 waves, 3-slot ring (the tiles that won on some ResNet-50
 // layer in profiles/conv_igemm_*; 128x256 / 256x128 with 4 waves spill and never won)
@@ -936,10 +1113,16 @@ constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2, 0},  {128, 128, 2, 4, 2, 0}, {64, 25
                          {128, 256, 2, 8, 3, 0}, {64, 256, 1, 8, 3, 0},  {256, 128, 4, 8, 3, 0},
                          {128, 256, 2, 8, 0, 0}, {64, 256, 1, 8, 0, 0},  {128, 128, 2, 4, 0, 0},
                          {256, 128, 4, 8, 0, 0}, {128, 128, 2, 4, 2, 1}, {256, 128, 4, 8, 3, 1},
-                         {128, 128, 2, 4, 2, 2}, {256, 128, 4, 8, 3, 2}};
+                         {128, 128, 2, 4, 2, 2}, {256, 128, 4, 8, 3, 2},
+                         // 14-21: stream-K work split of the generic / halo tiles above (make_plan)
+                         {128, 128, 2, 4, 2, 0, 1}, {256, 128, 4, 8, 3, 0, 1}, {128, 256, 2, 8, 3, 0, 1},
+                         {64, 256, 1, 8, 3, 0, 1},  {128, 256, 2, 8, 0, 0, 1}, {64, 256, 1, 8, 0, 0, 1},
+                         {128, 128, 2, 4, 0, 0, 1}, {256, 128, 4, 8, 0, 0, 1}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
+
+constexpr int kSkMaxBlocks = 4096;  // flag words the host keeps per device (damd_conv_sk_flag_words)
 
 int halo_lds_bytes(const Cfg& c, int W) {
   return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4;
@@ -959,6 +1142,16 @@ extern "C" {
 
 int damd_conv_num_cfgs() { return kNumCfgs; }
 
+// stream-K configs: fp32 slab workspace (floats) a launch needs, 0 for the others; the flag words
+// (kSkMaxBlocks, then one time-out counter) are a zeroed per-device buffer the caller keeps.
+int64_t damd_conv_sk_ws_floats(int K, int W, int cfg) {
+  if (cfg < 0 || cfg >= kNumCfgs || !kCfgs[cfg].sk) return 0;
+  const Cfg c = kCfgs[cfg];
+  return static_cast<int64_t>(256 * blocks_per_cu(c, W)) * c.bco * c.bp;
+}
+int damd_conv_sk_flag_words() { return kSkMaxBlocks + 16; }
+int damd_conv_cfg_is_sk(int cfg) { return cfg >= 0 && cfg < kNumCfgs && kCfgs[cfg].sk; }
+
 // Heuristic default config for a layer: widest co tile the channel count allows.
 int damd_conv_default_cfg(int K, int64_t M) {
   (void)M;
@@ -972,6 +1165,10 @@ int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, 
   if (cfg < 0 || cfg >= kNumCfgs) return 0;
   const Cfg c = kCfgs[cfg];
   if (!(C % kBK == 0 && C > 0 && K % c.bco == 0 && R * S <= 32)) return 0;
+  if (c.sk) {  // every XCD slice holds whole sets of co tiles: K / BCO divides the blocks per XCD
+    const int nblk = 256 * blocks_per_cu(c, W), ctiles = K / c.bco;
+    if (nblk % 8 != 0 || (nblk / 8) % ctiles != 0 || nblk > kSkMaxBlocks) return 0;
+  }
   if (c.nst == 0)
     return R == 3 && S == 3 && stride == 1 && pad == 1 && W >= 1 && halo_lds_bytes(c, W) <= kHaloMaxLds;
   return 1;
@@ -982,6 +1179,7 @@ int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
   const Cfg c = kCfgs[cfg];
   const int64_t ptiles = (M + c.bp - 1) / c.bp;
   const int ctiles = K / c.bco;
+  if (c.sk) return 256 * blocks_per_cu(c, W) / ctiles;  // the resident grid; plans may leave blocks idle
   int64_t groups = groups_override > 0 ? groups_override
                                        : (256LL * blocks_per_cu(c, W) + ctiles - 1) / ctiles;
   if (groups > ptiles) groups = ptiles;
@@ -1004,7 +1202,8 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          int R, int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi,
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
                          const float* scale, const float* shift, int pro, const void* p_res, const float* p_scale,
-                         const float* p_shift, const float* p_rscale, void* p_aout, uint8_t* p_mout) {
+                         const float* p_shift, const float* p_rscale, void* p_aout, uint8_t* p_mout, float* sk_ws,
+                         int* sk_flags) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
   if (pro < 0 || pro > 2) return -4;
   if (pro && (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg) || p_scale == nullptr || p_shift == nullptr ||
@@ -1026,52 +1225,56 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   g.ptiles = static_cast<int>((g.M + c.bp - 1) / c.bp);
   g.ctiles = K / c.bco;
   g.groups = groups;
+  if (c.sk && (sk_ws == nullptr || sk_flags == nullptr || groups != damd_conv_groups(g.M, K, W, cfg, 0))) return -5;
+  const SkArgs ska{sk_ws, sk_flags, sk_flags + kSkMaxBlocks};
   EpiArgs ea{static_cast<const bf16_t*>(d2), static_cast<const bf16_t*>(yb), mask, mean, scale, shift};
   const dim3 grid(static_cast<unsigned>(g.ctiles * groups));
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
-#define L1(BCO, BP, WCO, NW, NST, E, SC)                                                                  \
+#define L1(BCO, BP, WCO, NW, NST, E, SC, K_)                                                              \
   do {                                                                                                     \
     if constexpr (NST == 3 && SC == 0) {                                                                   \
       if (pro == 1) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 1>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 1, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
       if (pro == 2) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 2>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 2, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 0>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa); \
+    hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 0, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
   } while (0)
-#define LS(BCO, BP, WCO, NW, NST, SC)                          \
-  do {                                                         \
-    switch (epi) {                                             \
-      case 0: L1(BCO, BP, WCO, NW, NST, kEpiNone, SC); break;  \
-      case 1: L1(BCO, BP, WCO, NW, NST, kEpiStats, SC); break; \
-      case 2: L1(BCO, BP, WCO, NW, NST, kEpiBnbM, SC); break;  \
-      default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR, SC); break; \
-    }                                                          \
+#define LSK(BCO, BP, WCO, NW, NST, SC, K_)                          \
+  do {                                                              \
+    switch (epi) {                                                  \
+      case 0: L1(BCO, BP, WCO, NW, NST, kEpiNone, SC, K_); break;   \
+      case 1: L1(BCO, BP, WCO, NW, NST, kEpiStats, SC, K_); break;  \
+      case 2: L1(BCO, BP, WCO, NW, NST, kEpiBnbM, SC, K_); break;   \
+      default: L1(BCO, BP, WCO, NW, NST, kEpiBnbR, SC, K_); break;  \
+    }                                                               \
   } while (0)
+#define LS(BCO, BP, WCO, NW, NST, SC) LSK(BCO, BP, WCO, NW, NST, SC, 0)
 #define L(BCO, BP, WCO, NW, NST) LS(BCO, BP, WCO, NW, NST, 0)
   const int HR = halo_rows(c.bp, W);
   const int hlds = c.nst == 0 ? halo_lds_bytes(c, W) : 0;
-#define H1(BCO, BP, WCO, NW, E)                                                                              \
+#define H1(BCO, BP, WCO, NW, E, K_)                                                                          \
   do {                                                                                                       \
-    auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E>;                                                          \
+    auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_>;                                                      \
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR);                       \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska);                  \
   } while (0)
-#define H(BCO, BP, WCO, NW)                              \
-  do {                                                   \
-    switch (epi) {                                       \
-      case 0: H1(BCO, BP, WCO, NW, kEpiNone); break;     \
-      case 1: H1(BCO, BP, WCO, NW, kEpiStats); break;    \
-      case 2: H1(BCO, BP, WCO, NW, kEpiBnbM); break;     \
-      default: H1(BCO, BP, WCO, NW, kEpiBnbR); break;    \
-    }                                                    \
+#define HK(BCO, BP, WCO, NW, K_)                            \
+  do {                                                      \
+    switch (epi) {                                          \
+      case 0: H1(BCO, BP, WCO, NW, kEpiNone, K_); break;    \
+      case 1: H1(BCO, BP, WCO, NW, kEpiStats, K_); break;   \
+      case 2: H1(BCO, BP, WCO, NW, kEpiBnbM, K_); break;    \
+      default: H1(BCO, BP, WCO, NW, kEpiBnbR, K_); break;   \
+    }                                                       \
   } while (0)
+#define H(BCO, BP, WCO, NW) HK(BCO, BP, WCO, NW, 0)
   switch (cfg) {
     case 0: L(64, 128, 1, 4, 2); break;
     case 1: L(128, 128, 2, 4, 2); break;
@@ -1086,12 +1289,22 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
     case 10: LS(128, 128, 2, 4, 2, 1); break;
     case 11: LS(256, 128, 4, 8, 3, 1); break;
     case 12: LS(128, 128, 2, 4, 2, 2); break;
-    default: LS(256, 128, 4, 8, 3, 2); break;
+    case 13: LS(256, 128, 4, 8, 3, 2); break;
+    case 14: LSK(128, 128, 2, 4, 2, 0, 1); break;
+    case 15: LSK(256, 128, 4, 8, 3, 0, 1); break;
+    case 16: LSK(128, 256, 2, 8, 3, 0, 1); break;
+    case 17: LSK(64, 256, 1, 8, 3, 0, 1); break;
+    case 18: HK(128, 256, 2, 8, 1); break;
+    case 19: HK(64, 256, 1, 8, 1); break;
+    case 20: HK(128, 128, 2, 4, 1); break;
+    default: HK(256, 128, 4, 8, 1); break;
   }
 #undef L
 #undef LS
+#undef LSK
 #undef L1
 #undef H
+#undef HK
 #undef H1
   DAMD_CHECK_LAUNCH();
   return 0;

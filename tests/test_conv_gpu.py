@@ -94,3 +94,37 @@ def test_conv_wgrad_matches_fp32(ext, shape):
     dw32 = ext.conv_wgrad(x, dy, w.float(), st, pad, cfg0, 0)
     assert dw32.dtype == torch.float32
     torch.testing.assert_close(dw32, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+
+SK_TWIN = {14: 1, 15: 5, 16: 3, 17: 4, 18: 6, 19: 7, 20: 8, 21: 9}  # stream-K config -> whole-tile twin
+
+
+@pytest.mark.parametrize("shape", [(16, 256, 256, 3, 1, 14), (32, 512, 512, 3, 1, 7), (8, 1024, 256, 1, 1, 14),
+                                   (2, 64, 64, 3, 1, 9), (24, 2048, 512, 1, 1, 7), (4, 128, 128, 3, 1, 28)])
+def test_stream_k_configs_match_whole_tile_twins(ext, shape):
+    """Stream-K work split (tiles computed in segments by consecutive blocks, fp32 slabs handed
+    over in-launch): output and BN statistics vs fp32 and vs the same tile run whole; bitwise
+    reproducible launch to launch; no hand-off ever times out."""
+    n, cin, cout, k, st, hw = shape
+    pad = k // 2
+    torch.manual_seed(5)
+    x = cl(torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16))
+    w = cl((torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).to(torch.bfloat16))
+    ref = F.conv2d(x.float(), w.float(), stride=st, padding=pad)
+    ran = 0
+    for cfg, twin in SK_TWIN.items():
+        assert ext.conv_sk_cfg(cfg) and not ext.conv_sk_cfg(twin)
+        if not ext.conv_supported(x, w, cfg, st, pad):
+            continue
+        y, part = ext.conv_fwd(x, w, st, pad, True, cfg, 0)
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        yt, _ = ext.conv_fwd(x, w, st, pad, False, twin, 0)
+        torch.testing.assert_close(y.float(), yt.float(), rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+        tol = 2e-3 * ref.abs().sum((0, 2, 3)).max().item()
+        torch.testing.assert_close(part[:, 0].sum(0), ref.sum((0, 2, 3)), rtol=1e-3, atol=tol)
+        y2, part2 = ext.conv_fwd(x, w, st, pad, True, cfg, 0)
+        assert torch.equal(y2, y) and torch.equal(part2, part)
+        ran += 1
+    assert ran > 0
+    torch.cuda.synchronize()
+    assert ext.conv_sk_timeouts(x) == 0
