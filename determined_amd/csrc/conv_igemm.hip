@@ -919,17 +919,18 @@ struct WGeo {
   FastDiv dOHW, dOW;
 };
 
-template <int BCO, int BKC, int WCO, int NST = 2>
-__global__ void __launch_bounds__(kThreads, 2)
+template <int BCO, int BKC, int WCO, int NST = 2, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, 2)
 conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part, WGeo g) {
-  constexpr int WK = 4 / WCO;
+  constexpr int WK = NW / WCO;
   constexpr int TCO = BCO / WCO, TK = BKC / WK;
   constexpr int FI = TCO / 16, FJ = TK / 16;
-  static_assert(WCO * WK == 4 && FI >= 1 && FJ >= 1 && BCO % 64 == 0 && BKC % 64 == 0, "bad tile");
+  static_assert(WCO * WK == NW && FI >= 1 && FJ >= 1 && BCO % 64 == 0 && BKC % 64 == 0, "bad tile");
   constexpr int ACB = BCO / 64, BCB = BKC / 64;   // 64-channel blocks per operand
   constexpr int BLK = 64 * 64;                    // elements per [64 px][64 ch] block
   constexpr int STAGE = (ACB + BCB) * BLK;
-  constexpr int NI = (ACB + BCB) * 8 / 4;         // DMA instructions per wave per stage
+  static_assert((ACB + BCB) * 8 % NW == 0, "DMA pieces per wave");
+  constexpr int NI = (ACB + BCB) * 8 / NW;        // DMA instructions per wave per stage
   static_assert(NST == 2 || NST == 3, "ring depth");
   constexpr int NLW = NI;  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE];
@@ -959,7 +960,7 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
     const int p0 = p_begin + it * 64;
 #pragma unroll
     for (int n = 0; n < NI; ++n) {
-      const int ins = wave + 4 * n;               // 0 .. (ACB+BCB)*8-1
+      const int ins = wave + NW * n;              // 0 .. (ACB+BCB)*8-1
       const int blk = ins >> 3, row = 8 * (ins & 7) + prow;
       const int p = p0 + row;
       const int chunk = slot ^ swz_tr(row);
@@ -1321,12 +1322,15 @@ FastDiv make_fastdiv(uint32_t d) {
   return FastDiv{d, static_cast<uint32_t>(mul), l};
 }
 struct WCfg {
-  int bco, bkc, wco, nst;
+  int bco, bkc, wco, nst, nw = 4;
 };
 // 0: 128x128 (2x2 waves), 1: 64x128 (1x4), 2: 128x64 (4x1), 3: 64x64 (2x2: 32x32 per wave);
-// 4-7: the same tiles with a 3-slot ring
+// 4-7: the same tiles with a 3-slot ring; 8-11: 8-wave blocks with 256-wide tiles (1 block per CU):
+// each pixel chunk staged once feeds twice the MFMA work (the re-streaming of x / dY across
+// co / channel tiles through L2 is what bounds the small-spatial layers)
 constexpr WCfg kWCfgs[] = {{128, 128, 2, 2}, {64, 128, 1, 2}, {128, 64, 4, 2}, {64, 64, 2, 2},
-                           {128, 128, 2, 3}, {64, 128, 1, 3}, {128, 64, 4, 3}, {64, 64, 2, 3}};
+                           {128, 128, 2, 3}, {64, 128, 1, 3}, {128, 64, 4, 3}, {64, 64, 2, 3},
+                           {256, 256, 2, 2, 8}, {256, 128, 4, 3, 8}, {128, 256, 2, 3, 8}, {256, 128, 2, 3, 8}};
 constexpr int kNumWCfgs = sizeof(kWCfgs) / sizeof(kWCfgs[0]);
 }  // namespace
 
@@ -1343,7 +1347,8 @@ int damd_wgrad_supported(int C, int K, int cfg) {
 int damd_wgrad_splits(int64_t M, int C, int K, int R, int S, int cfg, int splits_override) {
   const WCfg c = kWCfgs[cfg];
   const int64_t tiles = static_cast<int64_t>(K / c.bco) * (R * S * C / c.bkc);
-  int64_t splits = splits_override > 0 ? splits_override : (512 + tiles - 1) / tiles;
+  const int64_t target = 256 * (8 / c.nw);  // resident blocks: 2 per CU at 4 waves, 1 at 8
+  int64_t splits = splits_override > 0 ? splits_override : (target + tiles - 1) / tiles;
   const int64_t max_splits = (M + 255) / 256;  // at least 4 k-steps per block
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1374,6 +1379,8 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
 #define WG(BCO, BKC, WCO, NST) \
   hipLaunchKernelGGL((conv_wgrad_kernel<BCO, BKC, WCO, NST>), grid, dim3(kThreads), 0, st, xp, dp, part, g)
+#define WG8(BCO, BKC, WCO, NST) \
+  hipLaunchKernelGGL((conv_wgrad_kernel<BCO, BKC, WCO, NST, 8>), grid, dim3(512), 0, st, xp, dp, part, g)
   switch (cfg) {
     case 0: WG(128, 128, 2, 2); break;
     case 1: WG(64, 128, 1, 2); break;
@@ -1382,9 +1389,14 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
     case 4: WG(128, 128, 2, 3); break;
     case 5: WG(64, 128, 1, 3); break;
     case 6: WG(128, 64, 4, 3); break;
-    default: WG(64, 64, 2, 3); break;
+    case 7: WG(64, 64, 2, 3); break;
+    case 8: WG8(256, 256, 2, 2); break;
+    case 9: WG8(256, 128, 4, 3); break;
+    case 10: WG8(128, 256, 2, 3); break;
+    default: WG8(256, 128, 2, 3); break;
   }
 #undef WG
+#undef WG8
   const int64_t n = static_cast<int64_t>(K) * R * S * C;  // multiple of 4 (C % 64 == 0)
   const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)

@@ -91,21 +91,49 @@ _TUNE: Dict[tuple, object] = {}
 _TUNE_ON = os.environ.get("DAMD_CONV_TUNE", "1") != "0"
 
 
-def _time_once(fn: Callable[[], object], reps: int = 3) -> float:
+def _parse_exclude(spec: str) -> frozenset:
+    """``DAMD_CONV_EXCLUDE="wgrad:8-11,*:14-21"``: candidates removed from the per-layer choice
+    (A/B measurements of new kernel configs on one box); ``*`` matches every key kind."""
+    out = set()
+    for tok in spec.split(","):
+        tok = tok.strip()
+        if not tok or ":" not in tok:
+            continue
+        kind, _, cfgs = tok.partition(":")
+        lo, _, hi = cfgs.partition("-")
+        if not lo.isdigit():
+            out.add((kind, cfgs))  # a named candidate ("miopen", "gemm")
+            continue
+        for c in range(int(lo), int(hi or lo) + 1):
+            out.add((kind, c))
+    return frozenset(out)
+
+
+_EXCLUDE = _parse_exclude(os.environ.get("DAMD_CONV_EXCLUDE", ""))
+
+
+def _time_once(fn: Callable[[], object], reps: int = 3, rounds: int = 2) -> float:
+    """Best of ``rounds`` timings of ``reps`` back-to-back calls (after one warm-up call)."""
     fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+    best = float("inf")
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / reps)
+    return best
 
 
 def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> object:
     got = _TUNE.get(key)
     if got is not None:
         return got
+    if _EXCLUDE:
+        kept = {c: f for c, f in cands.items() if (key[0], c) not in _EXCLUDE and ("*", c) not in _EXCLUDE}
+        cands = kept or cands
     if not _TUNE_ON or len(cands) <= 1 or torch.cuda.is_current_stream_capturing():
         choice = default if default in cands else next(iter(cands))
     else:

@@ -70,7 +70,8 @@ def test_conv_dgrad_via_flipped_weights(ext, shape):
     torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("shape", SHAPES + [(2, 64, 128, 3, 1, 23), (1, 128, 64, 1, 1, 40)])
+@pytest.mark.parametrize("shape", SHAPES + [(2, 64, 128, 3, 1, 23), (1, 128, 64, 1, 1, 40), (2, 256, 512, 3, 1, 9),
+                                   (3, 512, 256, 1, 1, 12)])
 def test_conv_wgrad_matches_fp32(ext, shape):
     n, cin, cout, k, st, hw = shape
     pad = k // 2

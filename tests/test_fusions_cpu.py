@@ -132,3 +132,10 @@ def test_chained_resnet_forward_equals_per_block_on_cpu(monkeypatch):
         outs.append((out.detach(), m.layer2[1].conv2.weight.grad.clone()))
     torch.testing.assert_close(outs[0][0], outs[1][0])
     torch.testing.assert_close(outs[0][1], outs[1][1])
+
+
+def test_conv_exclude_spec_parsing():
+    from determined_amd.ops.conv import _parse_exclude
+
+    ex = _parse_exclude("wgrad:8-10, *:14,fwd:miopen,bogus")
+    assert ex == frozenset({("wgrad", 8), ("wgrad", 9), ("wgrad", 10), ("*", 14), ("fwd", "miopen")})
