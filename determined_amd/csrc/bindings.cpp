@@ -63,6 +63,10 @@ extern "C" int damd_conv_default_cfg(int, int64_t);
 extern "C" int damd_conv_supported(int, int, int, int, int, int, int, int);
 extern "C" int damd_conv_groups(int64_t, int, int, int, int);
 extern "C" int damd_wgrad_num_cfgs();
+extern "C" int damd_wgrad3x3_supported(int, int, int, int);
+extern "C" int damd_wgrad3x3_splits(int64_t, int, int, int, int, int, int);
+extern "C" int damd_wgrad3x3_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int,
+                                    hipStream_t);
 extern "C" int damd_wgrad_supported(int, int, int);
 extern "C" int damd_wgrad_splits(int64_t, int, int, int, int, int, int);
 extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int, int,
@@ -954,6 +958,33 @@ at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tenso
   return dw;
 }
 
+// dW of a 3x3 / stride-1 / pad-1 convolution by the halo kernel (cfg 0: 128 output channels per
+// block, 1: 64), in w's dtype, channels-last [K, C, 3, 3].
+bool wgrad3x3_supported(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& w, int64_t cfg) {
+  return x.is_cuda() && x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+         dy.dim() == 4 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+         dy.size(1) == w.size(0) && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) && dy.size(3) == x.size(3) &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+         (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 &&
+         damd_wgrad3x3_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(x.size(3)),
+                                 static_cast<int>(cfg));
+}
+
+at::Tensor conv3x3_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& w, int64_t cfg, int64_t splits) {
+  TORCH_CHECK(wgrad3x3_supported(x, dy, w, cfg), "conv3x3_wgrad: unsupported input / config");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat, "conv3x3_wgrad: weight dtype");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+  const int sp = damd_wgrad3x3_splits(N, static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                      static_cast<int>(K), static_cast<int>(cfg), static_cast<int>(splits));
+  auto part = at::empty({sp, K * 9 * C}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({K, C, 3, 3}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = damd_wgrad3x3_launch(x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), dtype_code(w),
+                                      static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                      static_cast<int>(K), static_cast<int>(cfg), sp, cur_stream());
+  TORCH_CHECK(rc == 0, "conv3x3_wgrad: launch rejected");
+  return dw;
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -1136,6 +1167,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_bnact_fwd", &conv_bnact_fwd);
   m.def("conv_pro_supported", &conv_pro_supported);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
+  m.def("wgrad3x3_supported", &wgrad3x3_supported);
+  m.def("conv3x3_wgrad", &conv3x3_wgrad);
   m.def("conv_sk_timeouts", &conv_sk_timeouts);
   m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);

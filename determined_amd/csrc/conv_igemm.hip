@@ -1053,6 +1053,159 @@ conv_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, f
       }
 }
 
+// =========================================================== 3x3 / stride-1 halo weight gradient
+// dW[co][r][s][c] = sum_p dY[p][co] * x[p + (r-1, s-1)][c].  The generic weight gradient above
+// re-stages both operands for every (tap, channel block) column tile -- 9x the pixel traffic of a
+// 3x3 layer, and per-row im2col arithmetic.  Here one block owns a (BCO output channels) x (64
+// input channels) x (all 9 taps) tile and walks its pixel range once: per stage of 128 pixels it
+// stages the dY rows and the input halo (the 128 + 2(W+1) + 2 surrounding rows) once, and the 9
+// taps read the halo at row offsets r(W+1) + s.  Pixels are indexed on a zero-padded grid of
+// (H+1) x (W+1) per image (one pad column, one pad row): every out-of-image neighbour of a real
+// pixel lands on a pad position, which is staged as zeros, and pad positions carry zero dY -- so
+// no per-element boundary masks are needed (the cost: (H+1)(W+1)/(HW) more MFMA work, 1.15x at
+// 14x14, 1.04x at 56x56).  8 waves = 2 (output channels) x 4 (16 input channels each); fragments
+// by hardware-transposed LDS reads as in conv_wgrad_kernel; the pixel range is split over blocks
+// and the splits are summed by wgrad_finalize_kernel (deterministic).
+constexpr int kHwPB = 128;  // padded pixels per stage
+
+struct HWGeo {
+  int H, W, C, K;
+  int Mp;                          // N * (H + 1) * (W + 1)
+  int HR;                          // halo rows per stage (multiple of 8)
+  int cotiles, cblks, splits, chunk;
+  FastDiv dImg, dRow;              // (H + 1) * (W + 1), W + 1
+};
+
+template <int BCO>
+__global__ void __launch_bounds__(512, 2)
+conv3x3_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part,
+                     HWGeo g) {
+  constexpr int NW = 8;
+  constexpr int WCO = 2;                      // waves along output channels (x 4 along input channels)
+  constexpr int TCO = BCO / WCO, FI = TCO / 16;
+  constexpr int ACB = BCO / 64;               // 64-channel blocks of the dY image
+  constexpr int BLK = 64 * 64;
+  constexpr int DYS = 2 * ACB * BLK;          // dY image: [2 pixel halves][ACB][64 px][64 ch]
+  constexpr int NID = 2 * ACB * 8 / NW;       // dY DMA pieces per wave per stage
+  static_assert(FI >= 1 && NID >= 1, "bad tile");
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int SE = DYS + g.HR * 64;             // elements per stage
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c16 = lane & 15, lg = lane >> 4;
+  const int wco0 = (wave % WCO) * TCO, wc0 = (wave / WCO) * 16;
+
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ntile = g.cotiles * g.cblks;
+  const int tile = rid % ntile, split = rid / ntile;
+  const int cot = tile % g.cotiles, cb = tile / g.cotiles;
+  const int p_begin = split * g.chunk;
+  const int p_end = min(p_begin + g.chunk, g.Mp);
+  const int items = p_end > p_begin ? (p_end - p_begin + kHwPB - 1) / kHwPB : 0;
+  const int W1 = g.W + 1;
+
+  const int prow = lane >> 3, slot = lane & 7;
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+  // padded index -> element offset of the pixel in an [N][H][W] image, or -1 for a pad position
+  auto pix = [&](int q) -> int64_t {
+    if (q < 0 || q >= g.Mp) return -1;
+    const int n = static_cast<int>(g.dImg.div(static_cast<uint32_t>(q)));
+    const int rem = q - n * (g.H + 1) * W1;
+    const int h = static_cast<int>(g.dRow.div(static_cast<uint32_t>(rem)));
+    const int w = rem - h * W1;
+    if (h >= g.H || w >= g.W) return -1;
+    return (static_cast<int64_t>(n) * g.H + h) * g.W + w;
+  };
+  auto issue = [&](int stage, int it) {
+    bf16_t* base = lds + stage * SE;
+    const int q0 = p_begin + it * kHwPB;
+#pragma unroll
+    for (int n = 0; n < NID; ++n) {
+      const int ins = wave + NW * n;
+      const int blk = ins >> 3, row = 8 * (ins & 7) + prow;
+      const int pxb = blk / ACB, cob = blk - pxb * ACB;
+      const int q = q0 + 64 * pxb + row;
+      const int64_t e = q < p_end ? pix(q) : -1;
+      const bf16_t* src = e >= 0 ? dy + e * g.K + cot * BCO + cob * 64 + ((slot ^ swz_tr(row)) << 3) : zero;
+      dma16(src, base + blk * BLK + 8 * (ins & 7) * 64);
+    }
+    bf16_t* hx = base + DYS;
+    for (int k0 = 8 * wave; k0 < g.HR; k0 += 8 * NW) {
+      const int row = k0 + prow;
+      const int64_t e = pix(q0 - W1 - 1 + row);
+      const bf16_t* src = e >= 0 ? x + e * g.C + cb * 64 + ((slot ^ swz_tr(row)) << 3) : zero;
+      dma16(src, hx + k0 * 64);
+    }
+  };
+  // transposed fragment: channels col0 + c16 of rows r0..r0+3 and r0+16..r0+19 of a 64-wide image
+  auto tr_frag = [&](const bf16_t* img, int col0, int r0) {
+    const int q = c16 >> 2, pp = c16 & 3;
+    const int col = col0 + 4 * pp, chunk = col >> 3, within = col & 7;
+    const int ra = r0 + q, rb = r0 + 16 + q;
+    const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(img + ra * 64 + ((chunk ^ swz_tr(ra)) << 3) + within));
+    const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(img + rb * 64 + ((chunk ^ swz_tr(rb)) << 3) + within));
+    s8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  };
+
+  f4 acc[9][FI];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < FI; ++i) acc[t][i] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (items > 0) issue(0, 0);
+  for (int it = 0; it < items; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage it landed for every wave; stage it-1 is no longer read
+    if (it + 1 < items) issue((it + 1) & 1, it + 1);
+    const bf16_t* sd = lds + (it & 1) * SE;
+    const bf16_t* sx = sd + DYS;
+#pragma unroll
+    for (int kk = 0; kk < kHwPB / 32; ++kk) {
+      const int r0 = 32 * (kk & 1) + 4 * lg;  // row within the 64-pixel dY block
+      s8 a[FI];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int col = wco0 + 16 * i;
+        a[i] = tr_frag(sd + ((kk >> 1) * ACB + (col >> 6)) * BLK, col & 63, r0);
+      }
+      const int hr0 = 32 * kk + 4 * lg;       // halo row of pixel 32kk + 4lg for tap (0, 0)
+      // the tap row offsets are re-derived here from an opaque copy of W + 1: hoisted out of the
+      // pixel loop, the 72 per-(kk, tap) swizzled fragment addresses would spill the accumulators
+      int w1 = W1;
+      asm volatile("" : "+s"(w1));
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const s8 b = tr_frag(sx, wc0, hr0 + (t / 3) * w1 + (t % 3));
+#pragma unroll
+        for (int i = 0; i < FI; ++i) acc[t][i] = mfma(a[i], b, acc[t][i]);
+        // keep the scheduler from hoisting every tap's fragment reads (9 live fragments spill
+        // the 128-channel tile's 144 accumulator registers)
+        if (t % 3 == 2) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // acc[t][i][r] = partial dW[co = cot*BCO + wco0 + 16i + 4lg + r][tap t][c = cb*64 + wc0 + c16]
+  const int64_t Ktot = 9LL * g.C;
+  float* dst = part + static_cast<int64_t>(split) * g.K * Ktot;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t co = static_cast<int64_t>(cot) * BCO + wco0 + 16 * i + 4 * lg + r;
+        dst[co * Ktot + t * g.C + cb * 64 + wc0 + c16] = acc[t][i][r];
+      }
+}
+
 // dW = sum over splits of part[split][n].  A 256-thread block owns 64 float4 columns; its 4 waves
 // each sum every 4th split with 4 independent accumulators (16 loads in flight per wave instead
 // of one dependent chain per column), then the 4 wave sums are combined in LDS in a fixed order
@@ -1398,6 +1551,74 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
 #undef WG
 #undef WG8
   const int64_t n = static_cast<int64_t>(K) * R * S * C;  // multiple of 4 (C % 64 == 0)
+  const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
+  else
+    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
+  DAMD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+
+// ---- 3x3 halo weight gradient (cfg 0: 128 output channels per block, 1: 64)
+namespace {
+int hw_bco(int cfg) { return cfg == 0 ? 128 : 64; }
+int hw_halo_rows(int W) { return (kHwPB + 2 * (W + 1) + 2 + 7) / 8 * 8; }
+int hw_lds_bytes(int bco, int W) { return 2 * (2 * (bco / 64) * 64 * 64 + hw_halo_rows(W) * 64) * 2; }
+}  // namespace
+
+extern "C" {
+
+int damd_wgrad3x3_supported(int C, int K, int W, int cfg) {
+  if (cfg < 0 || cfg > 1) return 0;
+  const int bco = hw_bco(cfg);
+  return C % 64 == 0 && K % bco == 0 && W >= 1 && hw_lds_bytes(bco, W) <= 160 * 1024;
+}
+
+int damd_wgrad3x3_splits(int64_t N, int H, int W, int C, int K, int cfg, int splits_override) {
+  const int64_t tiles = static_cast<int64_t>(K / hw_bco(cfg)) * (C / 64);
+  int64_t splits = splits_override > 0 ? splits_override : (256 + tiles - 1) / tiles;
+  const int64_t Mp = N * (H + 1) * (W + 1);
+  const int64_t max_splits = (Mp + 4 * kHwPB - 1) / (4 * kHwPB);  // at least 4 stages per block
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  return static_cast<int>(splits);
+}
+
+// x: [N, H, W, C]; dy: [N, H, W, K] (stride 1, pad 1); part: [splits][K][9*C] fp32; dw: [K][3][3][C]
+int damd_wgrad3x3_launch(const void* x, const void* dy, float* part, void* dw, int w_dtype, int N, int H, int W,
+                         int C, int K, int cfg, int splits, hipStream_t st) {
+  if (!damd_wgrad3x3_supported(C, K, W, cfg)) return -1;
+  const int64_t Mp = static_cast<int64_t>(N) * (H + 1) * (W + 1);
+  if (Mp >= (int64_t{1} << 31) - 4096) return -2;
+  const int bco = hw_bco(cfg);
+  HWGeo g;
+  g.H = H; g.W = W; g.C = C; g.K = K;
+  g.Mp = static_cast<int>(Mp);
+  g.HR = hw_halo_rows(W);
+  g.cotiles = K / bco;
+  g.cblks = C / 64;
+  g.splits = splits;
+  g.chunk = static_cast<int>(((Mp + splits - 1) / splits + kHwPB - 1) / kHwPB * kHwPB);
+  g.dImg = make_fastdiv(static_cast<uint32_t>((H + 1) * (W + 1)));
+  g.dRow = make_fastdiv(static_cast<uint32_t>(W + 1));
+  const dim3 grid(static_cast<unsigned>(g.cotiles * g.cblks * splits));
+  const int lds = hw_lds_bytes(bco, W);
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* dp = static_cast<const bf16_t*>(dy);
+  if (cfg == 0) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<128>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, grid, dim3(512), lds, st, xp, dp, part, g);
+  } else {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<64>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, grid, dim3(512), lds, st, xp, dp, part, g);
+  }
+  const int64_t n = static_cast<int64_t>(K) * 9 * C;
   const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)
     hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));

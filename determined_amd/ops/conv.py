@@ -188,8 +188,8 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
-    """Weight gradient: conv_igemm.hip's split-pixel kernel or MIOpen, whichever timed faster for
-    this shape."""
+    """Weight gradient: conv_igemm.hip's split-pixel kernel, its 3x3 halo kernel (stride-1 3x3) or
+    MIOpen, whichever timed faster for this shape."""
     from determined_amd import ops
 
     e = ops.ext()
@@ -202,6 +202,10 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
     for c in range(e.wgrad_num_cfgs()):
         if e.wgrad_supported(x, dy, w.shape[0], c):
             cands[c] = (lambda c=c: e.conv_wgrad(x, dy, w, stride, pad, c, 0))
+    if stride == 1 and pad == 1 and w.shape[2] == 3 and w.shape[3] == 3:  # 3x3 halo kernel
+        for c in (0, 1):
+            if e.wgrad3x3_supported(x, dy, w, c):
+                cands[f"h{c}"] = (lambda c=c: e.conv3x3_wgrad(x, dy, w, c, 0))
     cands["miopen"] = miopen
     key = ("wgrad", tuple(x.shape), tuple(w.shape), stride, pad)
     return cands[_pick(key, cands, default="miopen")]()

@@ -134,6 +134,12 @@ def main():
                     got = e.conv_wgrad(xs, dys, w, st, pad, cfg, 0).float()
                     rec["wgrad_err"][str(cfg)] = round(((got - refw).norm() / refw.norm()).item(), 5)
                     rec["ours_wgrad_us"][str(cfg)] = round(timeit(lambda: e.conv_wgrad(x, dyw, w, st, pad, cfg, 0)), 1)
+            if k == 3 and st == 1:  # 3x3 halo weight gradient
+                for c in (0, 1):
+                    if e.wgrad3x3_supported(x, dyw, w, c):
+                        got = e.conv3x3_wgrad(xs, dys, w, c, 0).float()
+                        rec["wgrad_err"][f"h{c}"] = round(((got - refw).norm() / refw.norm()).item(), 5)
+                        rec["ours_wgrad_us"][f"h{c}"] = round(timeit(lambda: e.conv3x3_wgrad(x, dyw, w, c, 0)), 1)
             if rec["ours_wgrad_us"]:
                 tot["miopen_wgrad"] += rec["miopen_wgrad_us"] * cnt
                 tot["ours_wgrad"] += min(min(rec["ours_wgrad_us"].values()), rec["miopen_wgrad_us"]) * cnt

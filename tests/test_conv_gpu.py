@@ -129,3 +129,28 @@ def test_stream_k_configs_match_whole_tile_twins(ext, shape):
     assert ran > 0
     torch.cuda.synchronize()
     assert ext.conv_sk_timeouts(x) == 0
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 9), (3, 128, 128, 7), (1, 256, 128, 14), (2, 64, 128, 23),
+                                   (4, 512, 512, 7), (1, 128, 64, 57)])
+def test_conv3x3_halo_wgrad_matches_fp32(ext, shape):
+    """3x3 halo weight gradient (zero-padded pixel grid, 9 taps from one staged halo) vs fp32,
+    every config and forced split counts; bf16 and fp32 weight outputs."""
+    n, cin, cout, hw = shape
+    torch.manual_seed(7)
+    x = cl(torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16))
+    w = cl(torch.randn(cout, cin, 3, 3, device="cuda").to(torch.bfloat16))
+    dy = cl(torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16))
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), stride=1, padding=1)
+    ran = 0
+    for cfg in (0, 1):
+        if not ext.wgrad3x3_supported(x, dy, w, cfg):
+            continue
+        for splits in (0, 1, 5):
+            dw = ext.conv3x3_wgrad(x, dy, w, cfg, splits)
+            assert dw.shape == w.shape and dw.dtype == w.dtype and dw.is_contiguous(memory_format=torch.channels_last)
+            torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        dw32 = ext.conv3x3_wgrad(x, dy, w.float(), cfg, 0)
+        torch.testing.assert_close(dw32, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+        ran += 1
+    assert ran > 0
