@@ -72,14 +72,22 @@ class CheckpointContext:
             if ckpt_dir is None:
                 raise RuntimeError("ckpt_dir is required for .upload(shard=False)")
             storage_id = str(uuid.uuid4())
+        else:
+            storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
+        self._upload_as(storage_id, ckpt_dir, metadata, shard, selector)
+        return storage_id
+
+    def _upload_as(self, storage_id: str, ckpt_dir: Optional[os.PathLike], metadata: Optional[Dict[str, Any]],
+                   shard: bool, selector: Optional[Callable[[str], bool]]) -> None:
+        if not shard:
+            assert ckpt_dir is not None
             self._write_metadata_file(ckpt_dir, metadata or {})
             resources = storage.list_directory(ckpt_dir)
             if selector is not None:
                 resources = {k: v for k, v in resources.items() if selector(k) or k == "metadata.json"}
             self._storage_manager.upload(src=ckpt_dir, dst=storage_id, paths=sorted(resources))
             self._report_checkpoint(storage_id, resources, metadata or {})
-            return storage_id
-        storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
+            return
         resources: Dict[str, int] = {}
         self._dist.allgather_local(None)  # every local rank finished writing before anyone lists
         if ckpt_dir is not None:
@@ -101,7 +109,6 @@ class CheckpointContext:
                 self._storage_manager.upload(src=td, dst=storage_id, paths=["metadata.json"])
             merged_res["metadata.json"] = len(json.dumps(merged_md))
             self._report_checkpoint(storage_id, merged_res, merged_md)
-        return storage_id
 
     def _merge(self, metadata: Optional[Dict[str, Any]], resources: Dict[str, int]):
         all_md = self._dist.allgather(metadata or {})
@@ -146,6 +153,12 @@ class CheckpointContext:
             raise RuntimeError("cannot call .store_path(shard=False) from non-chief worker")
         storage_id = str(uuid.uuid4()) if not shard else self._dist.broadcast(
             str(uuid.uuid4()) if self._dist.rank == 0 else None)
+        if not getattr(self._storage_manager, "is_local", True):
+            # object store: stage locally, then upload like .upload() (metadata, shard merge, report)
+            with tempfile.TemporaryDirectory() as td:
+                yield pathlib.Path(td), storage_id
+                self._upload_as(storage_id, td, metadata, shard, None)
+            return
         with self._storage_manager.store_path(storage_id) as path:
             yield pathlib.Path(path), storage_id
             resources = storage.list_directory(path)

@@ -1,8 +1,9 @@
 """Checkpoint storage managers (reference: ``harness/determined/common/storage``).
 
 ``shared_fs`` and ``directory`` are filesystem-backed (the MI355X node's local NVMe or a shared
-mount).  ``s3`` / ``gcs`` / ``azure`` need their cloud SDKs, which are not installed in this
-image: building one raises a clear error instead of failing later.
+mount).  ``s3`` / ``gcs`` / ``azure`` talk to the object stores' HTTP APIs directly
+(``storage/cloud.py``: SigV4 / OAuth bearer / SharedKey signing) since the cloud SDKs are not part
+of this image.
 """
 
 import contextlib
@@ -133,27 +134,6 @@ class DirectoryStorageManager(SharedFSStorageManager):
         return cls(cfg["container_path"])
 
 
-class _MissingSDKStorage(StorageManager):
-    kind = ""
-    sdk = ""
-
-    def __init__(self, *a: Any, **kw: Any) -> None:
-        raise RuntimeError(f"checkpoint_storage type '{self.kind}' needs the {self.sdk} package, which is not "
-                           "installed in this environment; use shared_fs or directory")
-
-
-class S3StorageManager(_MissingSDKStorage):
-    kind, sdk = "s3", "boto3"
-
-
-class GCSStorageManager(_MissingSDKStorage):
-    kind, sdk = "gcs", "google-cloud-storage"
-
-
-class AzureStorageManager(_MissingSDKStorage):
-    kind, sdk = "azure", "azure-storage-blob"
-
-
 def build(cfg: Dict[str, Any], container_path: Optional[str] = None) -> StorageManager:
     t = cfg.get("type")
     if t == "shared_fs":
@@ -161,17 +141,28 @@ def build(cfg: Dict[str, Any], container_path: Optional[str] = None) -> StorageM
     if t == "directory":
         return DirectoryStorageManager.from_config(cfg, container_path)
     if t == "s3":
-        return S3StorageManager()
+        return S3StorageManager.from_config(cfg)
     if t == "gcs":
-        return GCSStorageManager()
+        return GCSStorageManager.from_config(cfg)
     if t == "azure":
-        return AzureStorageManager()
+        return AzureStorageManager.from_config(cfg)
     raise ValueError(f"unknown checkpoint_storage type {t!r}")
 
 
 def from_string(s: str) -> StorageManager:
-    if s.startswith("s3://"):
-        return S3StorageManager()
-    if s.startswith("gs://"):
-        return GCSStorageManager()
+    """``s3://bucket/prefix``, ``gs://bucket/prefix`` or a local directory (Core API v2 / unmanaged)."""
+    for scheme, cls in (("s3://", S3StorageManager), ("gs://", GCSStorageManager)):
+        if s.startswith(scheme):
+            bucket, _, prefix = s[len(scheme):].partition("/")
+            return cls(bucket, prefix=prefix) if cls is GCSStorageManager else cls(bucket, prefix=prefix,
+                                                                                   endpoint_url=os.environ.get(
+                                                                                       "AWS_ENDPOINT_URL"))
     return SharedFSStorageManager(os.path.expanduser(s))
+
+
+from determined_amd.storage.cloud import (  # noqa: E402
+    AzureStorageManager,
+    CloudStorageManager,
+    GCSStorageManager,
+    S3StorageManager,
+)
