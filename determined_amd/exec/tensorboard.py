@@ -183,7 +183,18 @@ def resolve_runs(master: Optional[str], token: Optional[str], exp_ids: List[int]
         st = cfg.get("tensorboard_storage") or cfg["checkpoint_storage"]
         from determined_amd import storage
 
-        return pathlib.Path(storage.build(st)._base_path) / "tensorboard" / "experiment" / str(eid)
+        sm = storage.build(st)
+        rel = f"tensorboard/experiment/{eid}"
+        if not getattr(sm, "is_local", True):  # object store: fetch the event files once
+            import tempfile
+
+            local = pathlib.Path(tempfile.mkdtemp(prefix=f"tb-exp-{eid}-"))
+            try:
+                sm.download(rel, local)
+            except FileNotFoundError:
+                pass
+            return local
+        return pathlib.Path(sm._base_path) / rel
 
     for eid in exp_ids:
         runs[f"exp-{eid}"] = base_of(eid)

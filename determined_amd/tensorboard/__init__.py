@@ -131,6 +131,20 @@ class TensorboardManager:
              mangler: Callable[[pathlib.Path, int], pathlib.Path] = lambda p, __: p, rank: int = 0) -> None:
         if self._sm is None:
             return
+        if not getattr(self._sm, "is_local", True):  # object store: upload the (mangled) event files
+            import tempfile
+
+            with tempfile.TemporaryDirectory() as td:
+                rels = []
+                for p in self.base_path.rglob("*"):
+                    if p.is_file() and selector(p):
+                        rel = mangler(p.relative_to(self.base_path), rank)
+                        (pathlib.Path(td) / rel).parent.mkdir(parents=True, exist_ok=True)
+                        shutil.copy2(p, pathlib.Path(td) / rel)
+                        rels.append(str(rel))
+                if rels:
+                    self._sm.upload(td, self._sync_path, paths=rels)
+            return
         target = pathlib.Path(self._sm._base_path) / self._sync_path
         for p in self.base_path.rglob("*"):
             if p.is_file() and selector(p):
