@@ -117,6 +117,7 @@ class Master:
         self.experiments: Dict[int, ExperimentRec] = {}
         self._order = 0
         self._closed = False
+        self._init_stream()
         self._restore()
         self._ticker = threading.Thread(target=self._tick_loop, daemon=True, name="master-tick")
         self._ticker.start()
@@ -126,6 +127,49 @@ class Master:
         with self.lock:
             self._closed = True
             self.cv.notify_all()
+        with self.stream_cv:
+            self.stream_cv.notify_all()
+
+    # ================================================================ event stream
+    # Reference: master/internal/stream (websocket subscriptions to entity changes).  Every write to
+    # a streamed table (_db.STREAMED) becomes an event {seq, ts, entity, id, fields}; clients long-poll
+    # GET /api/v1/stream?since=<seq> and get the newer events (or resync=true once the ring has
+    # dropped what they missed).  Large columns (configs, model definitions, snapshots) stay out.
+    _STREAM_SKIP = {"config", "model_def", "searcher_snapshot", "searcher_state", "metadata", "resources",
+                    "batch_metrics", "proxy"}
+
+    def _init_stream(self, capacity: int = 20000) -> None:
+        import collections
+
+        self.stream_cv = threading.Condition()
+        self.stream_events: "collections.deque" = collections.deque(maxlen=capacity)
+        self.stream_seq = 0
+
+        def on_change(table: str, key: Any, cols: Dict[str, Any]) -> None:
+            from determined_amd.master._db import STREAMED
+
+            fields = {k: v for k, v in cols.items() if k not in self._STREAM_SKIP and not isinstance(v, bytes)}
+            if table == "metrics":
+                key = cols.get("trial_id")
+            with self.stream_cv:
+                self.stream_seq += 1
+                self.stream_events.append({"seq": self.stream_seq, "ts": time.time(), "entity": STREAMED[table],
+                                           "id": key, "fields": fields})
+                self.stream_cv.notify_all()
+
+        self.db.on_change = on_change
+
+    def stream(self, since: int, timeout: float = 0.0, entities: Optional[List[str]] = None) -> Dict[str, Any]:
+        deadline = time.time() + timeout
+        with self.stream_cv:
+            while True:
+                oldest = self.stream_events[0]["seq"] if self.stream_events else self.stream_seq + 1
+                if since + 1 < oldest and since < self.stream_seq:
+                    return {"events": [], "last_seq": self.stream_seq, "resync": True}
+                evs = [e for e in self.stream_events if e["seq"] > since and (not entities or e["entity"] in entities)]
+                if evs or time.time() >= deadline or self._closed:
+                    return {"events": evs, "last_seq": self.stream_seq, "resync": False}
+                self.stream_cv.wait(max(0.0, min(1.0, deadline - time.time())))
 
     def _tick_loop(self) -> None:
         last_cleanup = 0.0

@@ -49,6 +49,10 @@ CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
 MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT"),
               ("models", "workspace", "TEXT DEFAULT 'Uncategorized'"), ("trials", "log_retention_days", "INTEGER")]
 
+# tables whose writes feed the master's event stream (GET /api/v1/stream, the web UI)
+STREAMED = {"experiments": "experiment", "trials": "trial", "checkpoints": "checkpoint", "tasks": "task",
+            "models": "model", "model_versions": "model_version", "metrics": "metrics"}
+
 JSON_COLS = {"config", "hparams", "metrics", "batch_metrics", "resources", "metadata", "searcher_snapshot", "labels",
              "searcher_state", "triggers", "proxy"}
 
@@ -67,6 +71,15 @@ class DB:
             except sqlite3.OperationalError:
                 pass
         self.lock = threading.RLock()
+        self.on_change = None  # callable(table, key, cols) for streamed tables (master event stream)
+
+    def _notify(self, table: str, key: Any, cols: Dict[str, Any]) -> None:
+        cb = self.on_change
+        if cb is not None and table in STREAMED:
+            try:
+                cb(table, key, cols)
+            except Exception:  # the stream is best effort; never fail a write for it
+                pass
 
     def _row(self, r: Optional[sqlite3.Row]) -> Optional[Dict[str, Any]]:
         if r is None:
@@ -99,7 +112,9 @@ class DB:
         with self.lock:
             cur = self.conn.execute(
                 f"INSERT INTO {table} ({','.join(keys)}) VALUES ({','.join('?' * len(keys))})", vals)
-            return int(cur.lastrowid)
+            rid = int(cur.lastrowid)
+        self._notify(table, cols.get("id", cols.get("uuid", rid)), cols)
+        return rid
 
     def update(self, table: str, key: str, key_val: Any, **cols: Any) -> None:
         if not cols:
@@ -109,6 +124,7 @@ class DB:
                 for k, v in cols.items()]
         with self.lock:
             self.conn.execute(f"UPDATE {table} SET {sets} WHERE {key}=?", vals + [key_val])
+        self._notify(table, key_val, cols)
 
     @staticmethod
     def now() -> float:

@@ -21,6 +21,7 @@ from determined_amd.master._iam import AuthError, _public_user
 from determined_amd.master._iam_routes import add_iam_routes
 from determined_amd.master._ntsc import add_ntsc_routes
 from determined_amd.master._exp_routes import add_exp_routes
+from determined_amd.master._webui import add_webui_routes
 from determined_amd.master._core import Master
 
 logger = logging.getLogger("determined_amd.master")
@@ -339,6 +340,11 @@ def build_routes(m: Master) -> List[Route]:
         return {"data": m.allocation_all_gather(aid, str(b["request_uuid"]), int(b["num_peers"]), b.get("data"),
                                                 b.get("rank"), float(b.get("timeout_seconds", 600)))}
 
+    @route("GET", "/api/v1/stream")
+    def stream(q, b):
+        ents = [e for e in q.get("entities", "").split(",") if e]
+        return m.stream(int(q.get("since", 0)), min(float(q.get("timeout_seconds", 0)), 60.0), ents or None)
+
     @route("GET", "/api/v1/allocations")
     def allocs(q, b):
         return {"allocations": [a.to_dict() for a in m.allocations.values() if a.state != "TERMINATED"]}
@@ -560,6 +566,7 @@ def build_routes(m: Master) -> List[Route]:
         lines += [f'det_experiments{{state="{r["state"]}"}} {r["n"]}' for r in exps]
         return _Raw("\n".join(lines) + "\n", "text/plain; version=0.0.4")
 
+    add_webui_routes(route, _Raw)
     return routes
 
 
