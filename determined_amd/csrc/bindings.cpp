@@ -76,6 +76,7 @@ extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int
                                     const float*, const float*, const float*, int, const void*, const float*,
                                     const float*, const float*, void*, uint8_t*, float*, int*);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
+extern "C" int damd_conv_pro_supported_w(int, int, int, int, int, int, int, int);
 extern "C" int64_t damd_conv_sk_ws_floats(int, int, int);
 extern "C" int damd_conv_sk_flag_words();
 extern "C" int damd_conv_cfg_is_sk(int);
@@ -813,10 +814,15 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
 // mask or an empty tensor).  stats: [4, C] of y's BatchNorm (mean, invstd, scale, shift).
 std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w, const c10::optional<at::Tensor>& res,
                                        const at::Tensor& stats, bool want_mask, int64_t cfg) {
-  TORCH_CHECK(conv_supported(y, w, cfg, 1, 0) && w.size(2) == 1 && w.size(3) == 1, "conv_bnact_fwd: unsupported input");
+  const int64_t R = w.size(2), S = w.size(3), pad = (R - 1) / 2;  // 1x1, or 3x3 / pad 1 (halo kernel)
+  TORCH_CHECK(R == S && (R == 1 || R == 3) && conv_supported(y, w, cfg, 1, pad), "conv_bnact_fwd: unsupported input");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3), K = w.size(0);
-  TORCH_CHECK(damd_conv_pro_supported(static_cast<int>(C), static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg)),
+  TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
+                                        static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(W),
+                                        static_cast<int>(cfg)),
               "conv_bnact_fwd: config has no prologue variant");
+  TORCH_CHECK(R == 1 || !(res.has_value() && res->defined()), "conv_bnact_fwd: no residual operand for 3x3 convs");
+  TORCH_CHECK(R == 1 || !want_mask, "conv_bnact_fwd: no ReLU mask output for 3x3 convs");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(0) == 4 && stats.size(1) == C &&
               stats.is_contiguous(), "conv_bnact_fwd: stats must be float32 [4, C]");
   const void* rp = nullptr;
@@ -836,7 +842,8 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
   const SkWorkspace sk = sk_workspace(y, K, W, cfg);
   const int rc = damd_conv_fwd_launch(y.data_ptr(), wl.data_ptr(), z.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
-                                      static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 1,
+                                      static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
+                                      static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), 1,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
                                       stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), nullptr, a.data_ptr(),
                                       want_mask ? mask.data_ptr<uint8_t>() : nullptr, sk.wsp, sk.flags);
@@ -845,9 +852,11 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
 }
 
 bool conv_pro_supported(const at::Tensor& y, const at::Tensor& w, int64_t cfg) {
-  return conv_supported(y, w, cfg, 1, 0) && w.size(2) == 1 && w.size(3) == 1 &&
-         damd_conv_pro_supported(static_cast<int>(y.size(1)), static_cast<int>(w.size(0)), 1, 1, 1, 0,
-                                 static_cast<int>(cfg));
+  const int64_t R = w.dim() == 4 ? w.size(2) : 0, pad = (R - 1) / 2;
+  return (R == 1 || R == 3) && w.size(3) == R && conv_supported(y, w, cfg, 1, pad) &&
+         damd_conv_pro_supported_w(static_cast<int>(y.size(1)), static_cast<int>(w.size(0)), static_cast<int>(R),
+                                   static_cast<int>(R), 1, static_cast<int>(pad), static_cast<int>(y.size(3)),
+                                   static_cast<int>(cfg));
 }
 
 // Stride-1 input gradient dX = conv(dY, wt, pad) (wt = flipped, transposed weights) of a conv
@@ -903,8 +912,9 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
                 "conv_dgrad_bn: pro_coef must be float32 [3, C]");
     TORCH_CHECK(pro_y->sizes() == dy.sizes() && pro_y->strides() == dy.strides() &&
                 pro_y->scalar_type() == at::kBFloat16, "conv_dgrad_bn: pro_y must match dy");
-    TORCH_CHECK(damd_conv_pro_supported(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
-                                        static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(cfg)),
+    TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
+                                          static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(W),
+                                          static_cast<int>(cfg)),
                 "conv_dgrad_bn: config has no prologue variant");
     pro = 2;
     p_res = pro_y->data_ptr();

@@ -728,10 +728,17 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 // rows starting at ANY row (the taps shift the fragment rows by r*W + s).
 constexpr int kHaloMaxLds = 160 * 1024;
 
-template <int BCO, int BP, int WCO, int NW, int EPI, int SK = 0>
+// PRO (as in conv_fwd_kernel): the halo is register-staged -- loaded at issue time, transformed
+// (PRO 1: a = relu(x * scale + shift), the consuming conv's BatchNorm+ReLU forward apply; PRO 2:
+// dy = A * dz + B * y + Cc, the producing conv's deferred BatchNorm-backward apply) and written to
+// LDS one iteration later; blocks of co tile 0 also store the operand for the tile's own pixels
+// (aout: the activation / gradient the weight gradient needs).  Out-of-image rows stay zero.
+constexpr int kHaloProRows = 6;  // register-staged halo rows per lane: HR <= 6 * 8 * NW
+
+template <int BCO, int BP, int WCO, int NW, int EPI, int SK = 0, int PRO = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk) {
+               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk, ProArgs pa) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -745,6 +752,7 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   bf16_t* halo = lds;               // [2][HR][64]
   bf16_t* wts = lds + 2 * HSLOT;    // [3][BCO][64]
   float* prm = reinterpret_cast<float*>(wts + 3 * WSLOT);
+  float* pprm = prm + 3 * BCO;      // PRO: [3][C] per input channel scale / shift / rscale
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rho = lane & 15, lg = lane >> 4;
@@ -765,6 +773,13 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
       prm[2 * BCO + t] = EPI == kEpiBnbR ? ea.shift[co] : 0.f;
     }
   }
+  if (PRO) {
+    for (int t = threadIdx.x; t < g.C; t += NT) {
+      pprm[t] = pa.scale[t];
+      pprm[g.C + t] = pa.shift[t];
+      pprm[2 * g.C + t] = PRO == 2 ? pa.rscale[t] : 0.f;
+    }
+  }
   const int prow = lane >> 3, slot = lane & 7;
   const bf16_t* wsrc[NIW];
 #pragma unroll
@@ -773,6 +788,49 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
   }
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+
+  // PRO: the pending register-staged halo (rows 8 * wave + 8 * NW * i + prow, channel chunk slot)
+  constexpr int MAXR = PRO ? kHaloProRows : 1;
+  bf16x8 hx[MAXR], hr[MAXR];
+  bf16_t* p_hs = nullptr;
+  int64_t p_f0 = 0;
+  int p_cb = 0;
+  bool p_pending = false;
+  auto flush = [&]() {
+    if (!PRO || !p_pending) return;
+    p_pending = false;
+    const float* sc = pprm + p_cb * kBK + (slot << 3);
+    float fs[8], fh[8], fr[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fs[e] = sc[e];
+      fh[e] = sc[g.C + e];
+      fr[e] = PRO == 2 ? sc[2 * g.C + e] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      if (8 * wave + 8 * NW * i >= HR) break;  // wave-uniform (HR % 8 == 0)
+      const int k = 8 * wave + 8 * NW * i + prow;
+      const int64_t f = p_f0 + k;
+      const bool valid = f >= 0 && f < g.M;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = PRO == 2 ? fs[e] * bf2f(hx[i].v[e]) + fr[e] * bf2f(hr[i].v[e]) + fh[e]
+                                 : fmaxf(bf2f(hx[i].v[e]) * fs[e] + fh[e], 0.f);
+        v[e] = valid ? t : 0.f;
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const u16v2_t pk = f2bf2(v[e], v[e + 1]);
+        o.v[e] = pk[0]; o.v[e + 1] = pk[1];
+      }
+      *reinterpret_cast<bf16x8*>(p_hs + k * kBK + ((slot ^ (k & 7)) << 3)) = o;
+      if (pa.aout != nullptr && ct == 0 && valid && k >= g.W + 1 && k < g.W + 1 + BP)
+        *reinterpret_cast<bf16x8*>(pa.aout + f * g.C + p_cb * kBK + (slot << 3)) = o;
+    }
+  };
 
   // load side: segment cursor (tile, channel-block range), tap, running halo count (slot parity)
   Cursor lc{0, 0, 0, 0, 0};
@@ -783,11 +841,27 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     if (l_tap == 0) {  // stage this tile's halo for channel block l_cb
       const int64_t f0 = static_cast<int64_t>(lc.pt) * BP - g.W - 1;
       bf16_t* hs = halo + (l_halo & 1) * HSLOT;
-      for (int k0 = 8 * wave; k0 < HR; k0 += 8 * NW) {
-        const int k = k0 + prow;
-        const int64_t f = f0 + k;
-        const bf16_t* src = (f >= 0 && f < g.M) ? x + f * g.C + l_cb * kBK + ((slot ^ (k & 7)) << 3) : zero;
-        dma16(src, hs + k0 * kBK);
+      if (PRO) {  // registers now, LDS at the next flush()
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const int k = 8 * wave + 8 * NW * i + prow;
+          const int64_t f = f0 + k;
+          const int64_t fc = (k < HR && f >= 0 && f < g.M) ? f : 0;  // clamped: zeroed at flush
+          const int64_t off = fc * g.C + l_cb * kBK + (slot << 3);
+          hx[i] = *reinterpret_cast<const bf16x8*>(x + off);
+          if (PRO == 2) hr[i] = *reinterpret_cast<const bf16x8*>(pa.res + off);
+        }
+        p_hs = hs;
+        p_f0 = f0;
+        p_cb = l_cb;
+        p_pending = true;
+      } else {
+        for (int k0 = 8 * wave; k0 < HR; k0 += 8 * NW) {
+          const int k = k0 + prow;
+          const int64_t f = f0 + k;
+          const bf16_t* src = (f >= 0 && f < g.M) ? x + f * g.C + l_cb * kBK + ((slot ^ (k & 7)) << 3) : zero;
+          dma16(src, hs + k0 * kBK);
+        }
       }
       ++l_halo;
     }
@@ -816,16 +890,27 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   uint32_t vm[FJ];  // per fragment pixel: bit 3r+s = tap (r, s) inside the image
 
   if (items > 0) issue(0);
+  if (PRO) {  // item 0's halo goes to LDS before the loop's first barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    flush();
+  }
   if (items > 1) issue(1);
   Cursor cc{0, 0, 0, 0, 0};
   seg_enter(cc, plan, g.cblk);
   int c_tap = 0, c_halo = 0;
   bool c_first = true;  // first item of a segment: per-pixel tap masks of its tile
   for (int it = 0; it < items; ++it) {
-    // the next item's DMAs may stay in flight (a halo issued with it is over-waited: correct)
-    if (it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the next item's DMAs may stay in flight (a halo issued with it is over-waited: correct;
+    // a register-staged halo (PRO) is waited for here and written to LDS by flush() below)
+    if (PRO) {
+      if (it + 1 < items) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(NIW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      if (it + 1 < items) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
+    flush();  // the halo of item it+1 (slot free: last read two units ago)
     if (it + 2 < items) issue((it + 2) % 3);
     const int64_t pt = cc.pt;
     if (c_first) {
@@ -1278,8 +1363,8 @@ int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
 
 constexpr int kSkMaxBlocks = 4096;  // flag words the host keeps per device (damd_conv_sk_flag_words)
 
-int halo_lds_bytes(const Cfg& c, int W) {
-  return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4;
+int halo_lds_bytes(const Cfg& c, int W, int C = 0) {  // C > 0: + the prologue's per-channel parameters
+  return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4 + 3 * C * 4;
 }
 
 int blocks_per_cu(const Cfg& c, int W = 0) {
@@ -1347,8 +1432,19 @@ int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
 int damd_conv_pro_supported(int C, int K, int R, int S, int stride, int pad, int cfg) {
   if (cfg < 0 || cfg >= kNumCfgs) return 0;
   const Cfg c = kCfgs[cfg];
+  if (c.nst == 0)  // 3x3 halo kernel: the 64-channel / 256-pixel 8-wave tiles (register-staged halo)
+    return c.bco == 64 && c.bp == 256 && c.nw == 8 && R == 3 && S == 3 && stride == 1 && pad == 1 &&
+           damd_conv_supported(C, K, R, S, stride, pad, 1, cfg);
   return c.nst == 3 && c.sch == 0 && R == 1 && S == 1 && stride == 1 && pad == 0 &&
          damd_conv_supported(C, K, R, S, stride, pad, 1, cfg);
+}
+
+// W-dependent limit of the halo prologue (the register-staged halo of one channel block)
+int damd_conv_pro_supported_w(int C, int K, int R, int S, int stride, int pad, int W, int cfg) {
+  if (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg)) return 0;
+  const Cfg c = kCfgs[cfg];
+  if (c.nst != 0) return 1;
+  return halo_rows(c.bp, W) <= kHaloProRows * 8 * c.nw && halo_lds_bytes(c, W, C) <= kHaloMaxLds;
 }
 
 // pro: the input is a = relu(x * p_scale + p_shift [+ p_res]) (ProArgs), 1x1 / stride 1 only
@@ -1360,7 +1456,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          int* sk_flags) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
   if (pro < 0 || pro > 2) return -4;
-  if (pro && (!damd_conv_pro_supported(C, K, R, S, stride, pad, cfg) || p_scale == nullptr || p_shift == nullptr ||
+  if (pro && (!damd_conv_pro_supported_w(C, K, R, S, stride, pad, W, cfg) || p_scale == nullptr || p_shift == nullptr ||
               (pro == 2 && (p_rscale == nullptr || p_res == nullptr))))
     return -4;
   const ProArgs pa{static_cast<const bf16_t*>(p_res), p_scale, p_shift, p_rscale, static_cast<bf16_t*>(p_aout), p_mout};
@@ -1412,12 +1508,20 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
 #define LS(BCO, BP, WCO, NW, NST, SC) LSK(BCO, BP, WCO, NW, NST, SC, 0)
 #define L(BCO, BP, WCO, NW, NST) LS(BCO, BP, WCO, NW, NST, 0)
   const int HR = halo_rows(c.bp, W);
-  const int hlds = c.nst == 0 ? halo_lds_bytes(c, W) : 0;
-#define H1(BCO, BP, WCO, NW, E, K_)                                                                          \
+  const int hlds = c.nst == 0 ? halo_lds_bytes(c, W, pro ? C : 0) : 0;
+#define H2(BCO, BP, WCO, NW, E, K_, P_)                                                                      \
   do {                                                                                                       \
-    auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_>;                                                      \
+    auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_, P_>;                                                  \
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska);                  \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa);              \
+  } while (0)
+#define H1(BCO, BP, WCO, NW, E, K_)                        \
+  do {                                                     \
+    if constexpr (BCO == 64 && BP == 256 && NW == 8) {     \
+      if (pro == 1) { H2(BCO, BP, WCO, NW, E, K_, 1); break; } \
+      if (pro == 2) { H2(BCO, BP, WCO, NW, E, K_, 2); break; } \
+    }                                                      \
+    H2(BCO, BP, WCO, NW, E, K_, 0);                        \
   } while (0)
 #define HK(BCO, BP, WCO, NW, K_)                            \
   do {                                                      \
@@ -1460,6 +1564,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
 #undef H
 #undef HK
 #undef H1
+#undef H2
   DAMD_CHECK_LAUNCH();
   return 0;
 }

@@ -112,6 +112,10 @@ def _parse_exclude(spec: str) -> frozenset:
 _EXCLUDE = _parse_exclude(os.environ.get("DAMD_CONV_EXCLUDE", ""))
 
 
+def _allowed(kind: str, cfg: object) -> bool:
+    return (kind, cfg) not in _EXCLUDE and ("*", cfg) not in _EXCLUDE
+
+
 def _time_once(fn: Callable[[], object], reps: int = 3, rounds: int = 2) -> float:
     """Best of ``rounds`` timings of ``reps`` back-to-back calls (after one warm-up call)."""
     fn()
@@ -318,7 +322,8 @@ class _LazyBNGrad:
 
 class _BNActConvFn(torch.autograd.Function):
     """``a = relu(bn(y) [+ residual])``, ``z = conv(a)`` (+ the BN statistic partials of z) as one
-    autograd node, so the backward can fuse the BN's reduce pass into the conv's input-gradient
+    autograd node (the forward apply inside the conv's operand staging where a prologue config
+    exists: 1x1 generic tiles, 3x3 halo tiles without a residual), so the backward can fuse the BN's reduce pass into the conv's input-gradient
     epilogue (conv_igemm.hip kEpiBnb*): the gradient at the BN output -- the conv's dX plus the
     gradient ``a`` received from its other consumer (a ResNet shortcut), ReLU-masked -- is
     written once together with its (sum, sum * (y - mean)) partials, and the BN backward is left
@@ -364,7 +369,8 @@ class _BNActConvFn(torch.autograd.Function):
         parked = _LazyBNGrad.take(g_z)  # g_z may be a deferred BN backward (the next BN's node)
         wt = _flip_weight(conv_w) if stride == 1 and 2 * pad == k - 1 else None
         fused = wt is not None and (mask is not None or not has_res)
-        pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(parked.dz, wt, c)]
+        pro_cfgs = ([c for c in range(e.conv_num_cfgs())
+                     if e.conv_pro_supported(parked.dz, wt, c) and _allowed("dgrad_bn_pro", c)]
                     if parked is not None and fused else [])
         if parked is not None and not pro_cfgs:
             g_z, parked = parked.materialise(), None
@@ -416,8 +422,10 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         st, pad = conv.stride[0], conv.padding[0]
         w = conv.weight
         lazy = bool(lazy_grad) and ops.fusion_enabled("bn_lazy_bwd")
-        pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
-                    if stats_part is not None and ops.fusion_enabled("bn_prologue") else [])
+        pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c) and _allowed("fwd_pro", c)]
+                    if stats_part is not None and ops.fusion_enabled("bn_prologue") and st == 1
+                    and 2 * pad == w.shape[2] - 1
+                    and (residual is None or w.shape[2] == 1) else [])  # 3x3 prologue: no residual
         if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
             key = ("fwd_pro", tuple(y.shape), tuple(w.shape), residual is not None)
             cfg = _TUNE.get(key)

@@ -561,3 +561,45 @@ def test_conv_dgrad_bn_with_deferred_bn_apply(ops):
         torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)  # fma order may differ by 1 ulp
         torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(part, part_ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64, 14), (2, 64, 128, 23), (1, 128, 64, 56)])
+def test_conv3x3_halo_prologues(ops, shape):
+    """3x3 halo kernel with a register-staged prologue: PRO 1 (BN+ReLU forward apply of the input,
+    `a` written for the weight gradient) vs bn_act_fwd + conv, and PRO 2 (deferred BN-backward
+    apply dy = A*dz + B*y + Cc) vs the kernel run on the explicitly applied dy."""
+    e = ops.ext()
+    torch.manual_seed(4)
+    cl = torch.channels_last
+    n, cin, cout, hw = shape
+    y = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") / (cin * 9) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    a_ref, stats, _ = e.bn_act_fwd(y, torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2,
+                                   None, None, 0.0, 1e-5, None, True, False, None)
+    z_ref = torch.nn.functional.conv2d(a_ref.float(), w.float(), padding=1)
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
+    assert cfgs, "no 3x3 prologue config"
+    for cfg in cfgs:
+        z, part, a, mask = e.conv_bnact_fwd(y, w, None, stats, False, cfg)
+        torch.testing.assert_close(a, a_ref, rtol=0, atol=0)
+        assert mask.numel() == 0
+        torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())
+        tol = 2e-3 * z_ref.abs().sum((0, 2, 3)).max().item()
+        torch.testing.assert_close(part[:, 0].sum(0), z_ref.sum((0, 2, 3)), rtol=1e-3, atol=tol)
+    # PRO 2 on the input gradient (flipped weights): dz of the next BN + its input y -> dy in staging
+    wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)  # [cin, cout, 3, 3]
+    dzn = torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yn = torch.randn_like(dzn)
+    coef = torch.randn(3, cout, device="cuda").contiguous()
+    yb = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    _, stb, _ = e.bn_act_fwd(yb, torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2,
+                             None, None, 0.0, 1e-5, None, True, False, None)
+    dy_ref = e.bn_bwd_apply_coef(dzn, yn, coef)
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(dzn, wt, c)]
+    assert cfgs
+    for cfg in cfgs:
+        dz_ref, part_ref = e.conv_dgrad_bn(dy_ref, wt, 1, cfg, None, yb, None, stb, None, None)
+        dz, part, dy = e.conv_dgrad_bn(dzn, wt, 1, cfg, None, yb, None, stb, yn, coef)
+        torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(part, part_ref, rtol=1e-3, atol=1e-2)
