@@ -101,6 +101,13 @@ def main() -> int:
         dt = float(t.item())
 
     loss = float(state["last_loss"]()) if "last_loss" in state else float("nan")
+    if rank == 0 and os.environ.get("DAMD_TUNE_DUMP"):  # per-layer kernel choices (A/B analysis)
+        from determined_amd.ops.conv import tuned_choices
+
+        with open(os.environ["DAMD_TUNE_DUMP"], "a") as f:
+            f.write(f"# DAMD_CONV_EXCLUDE={os.environ.get('DAMD_CONV_EXCLUDE', '')}\n")
+            for k, v in sorted(tuned_choices().items(), key=str):
+                f.write(f"{k} -> {v}\n")
     samples = a.batch * world * a.steps
     value = samples / dt
     if rank == 0:

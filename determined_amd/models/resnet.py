@@ -82,7 +82,7 @@ def _chain_blocks(blocks, x, split: bool):
     next block's first conv: the backward then fuses each BN's reduce pass into that conv's
     input-gradient epilogue.  Returns the last block's output.  Blocks expose ``convs``/``bns``
     (the main path, last BN takes the residual) and ``downsample``."""
-    # lazy: the pre-BN tensor came out of a bn_act_conv node whose conv is 1x1 / stride 1, which
+    # lazy: the pre-BN tensor came out of a bn_act_conv node whose conv is stride 1 (1x1 / 3x3), which
     # can absorb this BN's backward apply pass into its input gradient (ops/conv.py _LazyBNGrad)
     pending = None  # (pre-BN output, its stats partials, residual, BN, lazy) of the previous block
     for i, blk in enumerate(blocks):
@@ -105,8 +105,11 @@ def _chain_blocks(blocks, x, split: bool):
 
 
 def _pro_conv(conv: nn.Conv2d) -> bool:
-    """1x1 / stride-1 convs: their input gradient can absorb the following BN's backward apply."""
-    return conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0)
+    """Stride-1 1x1 and 3x3 (pad 1) convs: their input gradient can absorb the following BN's
+    backward apply (1x1: generic-tile prologue; 3x3: halo prologue where it times faster --
+    otherwise the parked gradient is materialised exactly as before)."""
+    k = conv.kernel_size
+    return conv.stride == (1, 1) and ((k == (1, 1) and conv.padding == (0, 0)) or (k == (3, 3) and conv.padding == (1, 1)))
 
 
 class BasicBlock(nn.Module):

@@ -116,6 +116,18 @@ def _allowed(kind: str, cfg: object) -> bool:
     return (kind, cfg) not in _EXCLUDE and ("*", cfg) not in _EXCLUDE
 
 
+def _prologue_pays(key: tuple, t_fused: Callable[[], float], t_plain: Callable[[], float]) -> bool:
+    """Whether a BN apply fused into a conv's operand staging beats the separate apply pass plus
+    the conv's best plain config for this layer (timed once, like the tile choice).  The 1x1
+    prologues always win (measured); the 3x3 halo prologue re-stages its halo per co tile and only
+    pays on some layers."""
+    got = _TUNE.get(key)
+    if got is None:
+        got = bool(_TUNE_ON and not torch.cuda.is_current_stream_capturing() and t_fused() < t_plain())
+        _TUNE[key] = got
+    return bool(got)
+
+
 def _time_once(fn: Callable[[], object], reps: int = 3, rounds: int = 2) -> float:
     """Best of ``rounds`` timings of ``reps`` back-to-back calls (after one warm-up call)."""
     fn()
@@ -372,6 +384,23 @@ class _BNActConvFn(torch.autograd.Function):
         pro_cfgs = ([c for c in range(e.conv_num_cfgs())
                      if e.conv_pro_supported(parked.dz, wt, c) and _allowed("dgrad_bn_pro", c)]
                     if parked is not None and fused else [])
+        if parked is not None and pro_cfgs and k != 1:
+            dzn, yn, coef = parked.dz, parked.y, parked.coef
+            plain_cfgs = _igemm_cfgs(e, dzn, wt, 1, k - 1 - pad)
+
+            def t_fused() -> float:
+                return min(_time_once(lambda c=c: e.conv_dgrad_bn(dzn, wt, k - 1 - pad, c, g_a, y, mask, stats, yn,
+                                                                  coef)) for c in pro_cfgs)
+
+            def t_plain() -> float:
+                gz = parked.materialise()
+                return _time_once(parked.materialise) + min(
+                    _time_once(lambda c=c: e.conv_dgrad_bn(gz, wt, k - 1 - pad, c, g_a, y, mask, stats, None, None))
+                    for c in plain_cfgs)
+
+            key = ("dgrad_pro_pays", tuple(dzn.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+            if not plain_cfgs or not _prologue_pays(key, t_fused, t_plain):
+                pro_cfgs = []
         if parked is not None and not pro_cfgs:
             g_z, parked = parked.materialise(), None
         if parked is None:
@@ -426,6 +455,22 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                     if stats_part is not None and ops.fusion_enabled("bn_prologue") and st == 1
                     and 2 * pad == w.shape[2] - 1
                     and (residual is None or w.shape[2] == 1) else [])  # 3x3 prologue: no residual
+        if pro_cfgs and w.shape[2] != 1:
+            dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
+            dummy[2].fill_(1.0)
+
+            def t_fused() -> float:
+                return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, None, dummy, False, c)) for c in pro_cfgs)
+
+            def t_plain() -> float:
+                apply = (lambda: e.bn_act_fwd(y, bn.weight, bn.bias, None, None, 0.0, float(bn.eps), None, True, True,
+                                              stats_part))
+                a0 = apply()[0]
+                return _time_once(apply) + min(_time_once(lambda c=c: e.conv_fwd(a0, w, st, pad, True, c, 0))
+                                               for c in _igemm_cfgs(e, a0, w, st, pad))
+
+            if not _prologue_pays(("fwd_pro_pays", tuple(y.shape), tuple(w.shape)), t_fused, t_plain):
+                pro_cfgs = []
         if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
             key = ("fwd_pro", tuple(y.shape), tuple(w.shape), residual is not None)
             cfg = _TUNE.get(key)
