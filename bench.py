@@ -43,6 +43,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--save-tune-db", default="", help="write the per-layer conv kernel choices after warm-up")
+    p.add_argument("--no-pretune", action="store_true",
+                   help="pick conv kernels inside the first warm-up step instead of a separate no-sync pass")
     p.add_argument("--conv-benchmark", type=int, default=1,
                    help="1: let MIOpen search for the fastest conv solvers (torch.backends.cudnn.benchmark)")
     return p.parse_args()
@@ -65,6 +68,10 @@ def main() -> int:
                                 use_harness=not a.no_harness)
 
     t_w = time.perf_counter()
+    if "tune" in state and not a.no_pretune:  # kernel choices outside the gradient all-reduce (all ranks alike)
+        state["tune"]()
+        if rank == 0:
+            print(f"[bench] conv kernels tuned ({time.perf_counter() - t_w:.1f}s)", file=sys.stderr, flush=True)
     # the first warm-up step may spend minutes in MIOpen's solver search for shapes missing from
     # the find-db: keep a heartbeat on stderr so supervisors do not mistake it for a hang
     import threading
@@ -84,6 +91,10 @@ def main() -> int:
             print(f"[bench] warmup {i + 1}/{a.warmup} {time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
     warm_done.set()
     torch.cuda.synchronize()
+    if a.save_tune_db and rank == 0:
+        from determined_amd.ops.conv import save_tune_db
+
+        print(f"[bench] saved {save_tune_db(a.save_tune_db)} conv choices to {a.save_tune_db}", file=sys.stderr)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -68,5 +68,22 @@ def harness_step(batch: int, variant: str, bucket_mb: float, device: torch.devic
             return float(state["metrics"][-1]["loss"].float().item())
         return float(state.get("last_report", {}).get("avg_metrics", {}).get("loss", float("nan")))
 
+    def tune() -> None:
+        """One forward/backward outside the gradient all-reduce (DDP no_sync, no optimizer step):
+        every conv layer picks its kernels (ops/conv.py) while no RCCL traffic shares the GPU, so
+        all ranks of a multi-GPU run time their candidates alike; gradients are dropped after."""
+        import contextlib
+
+        import torch.nn.functional as F
+
+        x, yl = pool[0]
+        sync_off = ctx._ddp[0].no_sync() if ctx._ddp else contextlib.nullcontext()
+        with sync_off:
+            F.cross_entropy(trial.model(trial._prep(x)).float(), yl).backward()
+        for m in ctx.models:
+            m.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+
     state["last_loss"] = last_loss
+    state["tune"] = tune
     return step, state

@@ -121,6 +121,10 @@ def _prologue_pays(key: tuple, t_fused: Callable[[], float], t_plain: Callable[[
     the conv's best plain config for this layer (timed once, like the tile choice).  The 1x1
     prologues always win (measured); the 3x3 halo prologue re-stages its halo per co tile and only
     pays on some layers."""
+    global _DB_LOADED
+    if not _DB_LOADED:
+        _DB_LOADED = True
+        load_tune_db()
     got = _TUNE.get(key)
     if got is None:
         got = bool(_TUNE_ON and not torch.cuda.is_current_stream_capturing() and t_fused() < t_plain())
@@ -143,9 +147,55 @@ def _time_once(fn: Callable[[], object], reps: int = 3, rounds: int = 2) -> floa
     return best
 
 
+# Per-layer choices measured once on an MI355X can be shipped as a file (like MIOpen's find-db):
+# DAMD_CONV_TUNE_DB=<path> (e.g. determined_amd/benchmarks/conv_tune_db.jsonl, ResNet-50 at batch
+# 512) starts from them -- warm-up 18 s instead of 70 s -- and shapes missing from it are timed as
+# before.  Off by default: the headline bench measured ~0.9% faster when the choices are timed in
+# the process that runs them (same box, interleaved A/B, profiles/conv_tune_db_ab_1gpu.txt).
+_DB_DEFAULT = ""
+_DB_LOADED = False
+
+
+def _tupled(v):
+    return tuple(_tupled(x) for x in v) if isinstance(v, list) else v
+
+
+def load_tune_db(path: Optional[str] = None) -> int:
+    """Merge a tuning database (JSON lines ``{"key": [...], "choice": ...}``) into the choices."""
+    path = os.environ.get("DAMD_CONV_TUNE_DB", _DB_DEFAULT) if path is None else path
+    if not path or not os.path.exists(path):
+        return 0
+    import json
+
+    n = 0
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            rec = json.loads(line)
+            _TUNE.setdefault(_tupled(rec["key"]), rec["choice"])
+            n += 1
+    return n
+
+
+def save_tune_db(path: str) -> int:
+    """Write the choices made so far (for ``load_tune_db``)."""
+    import json
+
+    with open(path, "w") as f:
+        for k, v in sorted(_TUNE.items(), key=str):
+            f.write(json.dumps({"key": k, "choice": v}) + "\n")
+    return len(_TUNE)
+
+
 def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> object:
+    global _DB_LOADED
+    if not _DB_LOADED:
+        _DB_LOADED = True
+        load_tune_db()
     got = _TUNE.get(key)
-    if got is not None:
+    if got is not None and (got in cands or isinstance(got, bool)):
         return got
     if _EXCLUDE:
         kept = {c: f for c, f in cands.items() if (key[0], c) not in _EXCLUDE and ("*", c) not in _EXCLUDE}
@@ -474,7 +524,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
             key = ("fwd_pro", tuple(y.shape), tuple(w.shape), residual is not None)
             cfg = _TUNE.get(key)
-            if cfg is None:  # tune on stand-in BN parameters (timing does not depend on them)
+            if cfg not in pro_cfgs:  # tune on stand-in BN parameters (timing does not depend on them)
                 dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
                 dummy[2].fill_(1.0)
                 cands = {c: (lambda c=c: e.conv_bnact_fwd(y, w, residual, dummy, residual is not None, c))
@@ -484,7 +534,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                                       pad, cfg, True, lazy)
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
         cfg = _TUNE.get(key)
-        if cfg is None:  # tune the conv on a stand-in input of the same shape
+        if not isinstance(cfg, int) or not e.conv_supported(y, w, cfg, st, pad):  # tune on a stand-in input
             cands = {c: (lambda c=c: e.conv_fwd(y, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, y, w, st, pad)}
             cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
         return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,

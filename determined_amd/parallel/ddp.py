@@ -216,6 +216,8 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._sync_enabled = prev
             self._reset_arrivals()
+            if self._steps == 0:  # bucket order is learned from the first SYNCED backward
+                self._observed = []
 
     def _reset_arrivals(self) -> None:
         for b in self._buckets:

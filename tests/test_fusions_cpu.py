@@ -139,3 +139,20 @@ def test_conv_exclude_spec_parsing():
 
     ex = _parse_exclude("wgrad:8-10, *:14,fwd:miopen,bogus")
     assert ex == frozenset({("wgrad", 8), ("wgrad", 9), ("wgrad", 10), ("*", 14), ("fwd", "miopen")})
+
+
+def test_conv_tune_db_roundtrip(tmp_path, monkeypatch):
+    import determined_amd.ops.conv as conv
+
+    monkeypatch.setattr(conv, "_TUNE", {("fwd", (512, 64, 56, 56), (64, 64, 3, 3), 1, 1): 7,
+                                        ("wgrad", (8, 64, 9, 9), (64, 64, 3, 3), 1, 1): "h1",
+                                        ("fwd_pro_pays", (512, 64, 56, 56), (64, 64, 3, 3)): True})
+    p = tmp_path / "db.jsonl"
+    assert conv.save_tune_db(str(p)) == 3
+    saved = dict(conv._TUNE)
+    monkeypatch.setattr(conv, "_TUNE", {})
+    assert conv.load_tune_db(str(p)) == 3
+    assert conv._TUNE == saved
+    # a shipped choice is used only if it is one of the candidates of this build
+    monkeypatch.setattr(conv, "_DB_LOADED", True)
+    assert conv._pick(("fwd", (512, 64, 56, 56), (64, 64, 3, 3), 1, 1), {3: None, 7: None}, 3) == 7

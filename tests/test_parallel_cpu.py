@@ -93,3 +93,30 @@ def test_ddp_single_process_grad_views():
     ddp.finish()
     ptrs = {b.buffer.data_ptr() for b in ddp._buckets}
     assert all(any(p.grad.data_ptr() >= bp for bp in ptrs) for p in m.parameters())
+
+
+def test_ddp_no_sync_before_first_step_keeps_bucket_order_clean():
+    """A gradient-less warm-up backward under no_sync (kernel tuning) must not leave its hook order
+    behind: the first synced step re-derives the buckets from its own order, each parameter once."""
+    import torch
+
+    from determined_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.0001, first_bucket_mb=0.0001)
+    x = torch.randn(5, 8)
+    with ddp.no_sync():
+        ddp(x).square().sum().backward()
+    ddp.zero_grad()
+    ddp(x).square().sum().backward()
+    ddp.finish()
+    ids = [id(p) for b in ddp._buckets for p in b.params]
+    assert len(ids) == len(set(ids)) == len(list(model.parameters()))
+    ref = torch.nn.Sequential(*[m for m in model])  # same module: grads must equal a plain backward
+    g = [p.grad.clone() for p in model.parameters()]
+    for p in model.parameters():
+        p.grad = None
+    ref(x).square().sum().backward()
+    for a, b in zip(g, [p.grad for p in model.parameters()]):
+        torch.testing.assert_close(a, b)
