@@ -63,6 +63,11 @@ extern "C" int damd_conv_default_cfg(int, int64_t);
 extern "C" int damd_conv_supported(int, int, int, int, int, int, int, int);
 extern "C" int damd_conv_groups(int64_t, int, int, int, int);
 extern "C" int damd_wgrad_num_cfgs();
+extern "C" int damd_conv1x1_bwd_fused_supported(int, int);
+extern "C" int damd_conv1x1_bwd_fused_blocks(int64_t);
+extern "C" int damd_conv1x1_bwd_fused_launch(const void*, const void*, const float*, const void*, const void*,
+                                             const void*, const float*, int64_t, void*, float*, float*, void*, int,
+                                             int, int, hipStream_t);
 extern "C" int damd_wgrad3x3_supported(int, int, int, int);
 extern "C" int damd_wgrad3x3_splits(int64_t, int, int, int, int, int, int);
 extern "C" int damd_wgrad3x3_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int,
@@ -995,6 +1000,45 @@ at::Tensor conv3x3_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Te
   return dw;
 }
 
+// Fused backward of z = conv1x1(a) (K = 256 <- C = 64), z's gradient a deferred BN backward
+// (dy = coef[0] * dzn + coef[1] * yn + coef[2]) and a = relu(bn(yb)) without a residual: returns
+// (dz = dX * relu'(bn(yb)), its BN-backward partials [G, 2, C], dW in w's dtype / layout).
+bool conv1x1_bwd_fused_supported(const at::Tensor& w) {
+  return w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 &&
+         damd_conv1x1_bwd_fused_supported(static_cast<int>(w.size(0)), static_cast<int>(w.size(1)));
+}
+
+std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& dzn, const at::Tensor& yn, const at::Tensor& coef,
+                                          const at::Tensor& w, const at::Tensor& a, const at::Tensor& yb,
+                                          const at::Tensor& stats) {
+  TORCH_CHECK(conv1x1_bwd_fused_supported(w), "conv1x1_bwd_fused: unsupported weight shape");
+  const int64_t K = w.size(0), C = w.size(1);
+  auto cl = at::MemoryFormat::ChannelsLast;
+  for (const at::Tensor* t : {&dzn, &yn, &a, &yb})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 4 && t->is_contiguous(cl) &&
+                (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "conv1x1_bwd_fused: bf16 channels-last inputs");
+  TORCH_CHECK(dzn.size(1) == K && yn.sizes() == dzn.sizes() && a.size(1) == C && yb.sizes() == a.sizes() &&
+              a.size(0) == dzn.size(0) && a.size(2) == dzn.size(2) && a.size(3) == dzn.size(3), "conv1x1_bwd_fused: shapes");
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.dim() == 2 && coef.size(0) == 3 && coef.size(1) == K &&
+              coef.is_contiguous(), "conv1x1_bwd_fused: coef must be float32 [3, K]");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(0) == 4 && stats.size(1) == C,
+              "conv1x1_bwd_fused: stats must be float32 [4, C]");
+  const int64_t M = a.size(0) * a.size(2) * a.size(3);
+  auto wt = w.reshape({K, C}).t().contiguous().to(at::kBFloat16);
+  auto bnp = at::stack({stats[0], stats[2], stats[3]}).contiguous();
+  const int G = damd_conv1x1_bwd_fused_blocks(M);
+  auto dzo = at::empty_like(yb);
+  auto part = at::empty({G, 2, C}, a.options().dtype(at::kFloat));
+  auto wpart = at::empty({G, K * C}, a.options().dtype(at::kFloat));
+  auto dw = at::empty({K, C, 1, 1}, w.options().memory_format(cl));
+  const int rc = damd_conv1x1_bwd_fused_launch(dzn.data_ptr(), yn.data_ptr(), coef.data_ptr<float>(), wt.data_ptr(),
+                                               a.data_ptr(), yb.data_ptr(), bnp.data_ptr<float>(), M, dzo.data_ptr(),
+                                               part.data_ptr<float>(), wpart.data_ptr<float>(), dw.data_ptr(),
+                                               dtype_code(w), static_cast<int>(K), static_cast<int>(C), cur_stream());
+  TORCH_CHECK(rc == 0, "conv1x1_bwd_fused: launch rejected");
+  return {dzo, part, dw};
+}
+
 // ---------------------------------------------------------------- flash attention
 // q, k, v, o, ... are [B, H, T, D] views (any batch/head/token strides, contiguous D,
 // 16-byte aligned rows); D in {64, 128}; bf16.
@@ -1178,6 +1222,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_pro_supported", &conv_pro_supported);
   m.def("conv_num_cfgs", &damd_conv_num_cfgs);
   m.def("wgrad3x3_supported", &wgrad3x3_supported);
+  m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported);
+  m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
   m.def("conv_sk_timeouts", &conv_sk_timeouts);
   m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });

@@ -1291,6 +1291,205 @@ conv3x3_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy
       }
 }
 
+// ==================================================== fused 1x1 backward (dgrad + wgrad, one pass)
+// The backward of z = conv1x1(a) when z's gradient arrives as a deferred BatchNorm backward
+// (dy = A*dz + B*y + Cc, ops/conv.py _LazyBNGrad) and a = relu(bn(yb)) without a residual: the
+// separate kernels read (dz, y) for the input gradient, write dy for the weight gradient, and read
+// dy and a again there -- on ResNet-50's 56x56 layers that is ~1.6 GB of the ~3.9 GB the two
+// passes move.  Here one persistent block per CU walks 64-pixel tiles once: it forms the dy tile
+// in LDS from (dz, y), computes the input gradient dX = dy . W (MFMA, the BN-backward epilogue:
+// dz' = dX * [yb * scale + shift > 0] and the (sum dz', sum dz' (yb - mean)) partials) and
+// accumulates dW += dy^T . a in registers; each block's dW partial is summed by
+// wgrad_finalize_kernel (deterministic).  K (dz channels) = 256, C (dX channels) = 64 -- the
+// 64 -> 256 bottleneck conv of ResNet-50's first stage, where the traffic is largest.
+template <int K, int C>
+__global__ void __launch_bounds__(512, 2)
+conv1x1_bwd_fused_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ yk, const float* __restrict__ coef,
+                         const bf16_t* __restrict__ wt, const bf16_t* __restrict__ a, const bf16_t* __restrict__ yb,
+                         const float* __restrict__ bnp, int M, bf16_t* __restrict__ dzo, float* __restrict__ part,
+                         float* __restrict__ wpart) {
+  constexpr int NW = 8, NT = 512, BP = 64;
+  constexpr int KB = K / 64;                    // 64-channel blocks of dy
+  constexpr int BLK = 64 * 64;
+  static_assert(C == 64 && K % 64 == 0 && KB * 8 % NW == 0, "tile");
+  // dgrad: out^T[c][px] = Wt[c][k] . dy^T[k][px]; waves 2 (c) x 4 (px): TCO 32, TP 16
+  constexpr int DWCO = 2, DTCO = C / DWCO, DFI = DTCO / 16;
+  // wgrad: dW[k][c] = dy^T[k][px] . a[px][c]; waves 4 (k) x 2 (c): TK = K / 4, TC 32
+  constexpr int WWK = 4, WTK = K / WWK, WFI = WTK / 16, WFJ = 2;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* wimg = lds;                           // [KB][64 c][64 k]     swz
+  bf16_t* dyimg = wimg + KB * BLK;              // [2][KB][64 px][64 k] swz
+  bf16_t* aimg = dyimg + 2 * KB * BLK;          // [2][64 px][64 c]     swz_tr
+  float* cf = reinterpret_cast<float*>(aimg + 2 * BLK);  // [3][K] A, B, Cc
+  float* prm = cf + 3 * K;                      // [3][C] mean, scale, shift of the BN on yb
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rho = lane & 15, lg = lane >> 4, c16 = rho;
+  const int prow = lane >> 3, slot = lane & 7;
+  const int tiles = (M + BP - 1) / BP;
+  const int G = gridDim.x, b = blockIdx.x;
+
+  // ---- once per block: weights (LDS-DMA, swizzled source), BN-backward coefficients, BN parameters
+#pragma unroll
+  for (int n = 0; n < KB * 8 / NW; ++n) {
+    const int piece = wave + NW * n;            // (k-block, 8-row group)
+    const int kb = piece >> 3, row = 8 * (piece & 7) + prow;
+    dma16(wt + static_cast<int64_t>(row) * K + kb * 64 + ((slot ^ swz(row)) << 3), wimg + kb * BLK + 8 * (piece & 7) * 64);
+  }
+  for (int t = threadIdx.x; t < 3 * K; t += NT) cf[t] = coef[t];
+  for (int t = threadIdx.x; t < 3 * C; t += NT) prm[t] = bnp[t];
+
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
+  // per-thread staging of one dy tile: pass kb covers k-block kb, thread -> (pixel t >> 3, chunk t & 7)
+  const int spx = threadIdx.x >> 3, sch = threadIdx.x & 7;
+  bf16x8 rz[KB], ry[KB], ryb;
+  const int dwco0 = (wave % DWCO) * DTCO, dwp0 = (wave / DWCO) * 16;
+  auto load_tile = [&](int tl, int buf) {
+    const int64_t p = static_cast<int64_t>(tl) * BP + spx;
+    const int64_t pc = p < M ? p : 0;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int64_t off = pc * K + kb * 64 + (sch << 3);
+      rz[kb] = *reinterpret_cast<const bf16x8*>(dz + off);
+      ry[kb] = *reinterpret_cast<const bf16x8*>(yk + off);
+    }
+    const int64_t pe = static_cast<int64_t>(tl) * BP + dwp0 + rho;  // this lane's epilogue pixel
+    ryb = *reinterpret_cast<const bf16x8*>(yb + (pe < M ? pe : 0) * C + dwco0 + 8 * lg);
+    const int arow = 8 * wave + prow;
+    const int64_t pa = static_cast<int64_t>(tl) * BP + arow;
+    dma16(pa < M ? a + pa * C + ((slot ^ swz_tr(arow)) << 3) : zero, aimg + buf * BLK + 8 * wave * 64);
+  };
+  auto store_tile = [&](int tl, int buf) {  // dy = A*dz + B*y + Cc -> LDS (zero past the last pixel)
+    const bool ok = static_cast<int64_t>(tl) * BP + spx < M;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const float* A = cf + kb * 64 + (sch << 3);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = ok ? A[e] * bf2f(rz[kb].v[e]) + A[K + e] * bf2f(ry[kb].v[e]) + A[2 * K + e] : 0.f;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const u16v2_t pk = f2bf2(v[e], v[e + 1]);
+        o.v[e] = pk[0]; o.v[e + 1] = pk[1];
+      }
+      *reinterpret_cast<bf16x8*>(dyimg + (buf * KB + kb) * BLK + spx * 64 + ((sch ^ swz(spx)) << 3)) = o;
+    }
+  };
+  // transposed fragment of a 64-wide image (rows r0..r0+3, r0+16..r0+19; column col0 + c16) under
+  // swizzle f: the dy image keeps the dgrad's b128 swizzle, the a image the wgrad's
+  auto tr_frag = [&](const bf16_t* img, int col0, int r0, bool dy_swz) {
+    const int q = c16 >> 2, pp = c16 & 3;
+    const int col = col0 + 4 * pp, chunk = col >> 3, within = col & 7;
+    const int ra = r0 + q, rb = r0 + 16 + q;
+    const int fa = dy_swz ? swz(ra) : swz_tr(ra), fb = dy_swz ? swz(rb) : swz_tr(rb);
+    const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + ra * 64 + ((chunk ^ fa) << 3) + within));
+    const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + rb * 64 + ((chunk ^ fb) << 3) + within));
+    s8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  };
+
+  f4 accw[WFI][WFJ];
+#pragma unroll
+  for (int i = 0; i < WFI; ++i)
+#pragma unroll
+    for (int j = 0; j < WFJ; ++j) accw[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float st_s[DFI / 2][8], st_q[DFI / 2][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { st_s[0][e] = 0.f; st_q[0][e] = 0.f; }
+  const int wk0 = (wave % WWK) * WTK, wc0 = (wave / WWK) * 32;
+
+  int buf = 0;
+  if (b < tiles) load_tile(b, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // coefficients / BN parameters in LDS before the first dy tile is formed
+  for (int tl = b; tl < tiles; tl += G) {
+    store_tile(tl, buf);
+    const bf16x8 yb_cur = ryb;
+    __syncthreads();  // dy tile, a tile (DMA waited by every wave), weights, coefficients visible
+    if (tl + G < tiles) load_tile(tl + G, buf ^ 1);
+    const bf16_t* dyb = dyimg + buf * KB * BLK;
+    // ---- input gradient for the 64 pixels x 64 channels, then the BN-backward epilogue
+    f4 acc[DFI];
+#pragma unroll
+    for (int i = 0; i < DFI; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + lg;
+        const int prw = dwp0 + rho;
+        const s8 bv = *reinterpret_cast<const s8*>(dyb + kb * BLK + prw * 64 + ((chunk ^ swz(prw)) << 3));
+#pragma unroll
+        for (int i = 0; i < DFI; ++i) {
+          const int row = dwco0 + a_row(i, rho);
+          const s8 av = *reinterpret_cast<const s8*>(wimg + kb * BLK + row * 64 + ((chunk ^ swz(row)) << 3));
+          acc[i] = mfma(av, bv, acc[i]);
+        }
+      }
+    {  // lane: channels dwco0 + 8lg .. +7 of pixel tl*64 + dwp0 + rho
+      const int64_t m = static_cast<int64_t>(tl) * BP + dwp0 + rho;
+      const int cl = dwco0 + 8 * lg;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { o[e] = acc[0][e]; o[4 + e] = acc[1][e]; }
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float yv = bf2f(yb_cur.v[e]);
+        o[e] = yv * prm[C + cl + e] + prm[2 * C + cl + e] > 0.f ? o[e] : 0.f;  // recomputed ReLU
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const u16v2_t pk = f2bf2(o[e], o[e + 1]);
+        v.v[e] = pk[0]; v.v[e + 1] = pk[1];
+      }
+      if (m < M) {
+        *reinterpret_cast<bf16x8*>(dzo + m * C + cl) = v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f(v.v[e]);  // the stored (rounded) dz', as the apply pass reads it
+          st_s[0][e] += f;
+          st_q[0][e] += f * (bf2f(yb_cur.v[e]) - prm[cl + e]);
+        }
+      }
+    }
+    // ---- weight gradient: dW[k][c] += dy^T . a over the tile's 64 pixels
+    const bf16_t* ab = aimg + buf * BLK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = 32 * kk + 4 * lg;
+      s8 av[WFI], bv[WFJ];
+#pragma unroll
+      for (int i = 0; i < WFI; ++i) {
+        const int col = wk0 + 16 * i;
+        av[i] = tr_frag(dyb + (col >> 6) * BLK, col & 63, r0, true);
+      }
+#pragma unroll
+      for (int j = 0; j < WFJ; ++j) bv[j] = tr_frag(ab, wc0 + 16 * j, r0, false);
+#pragma unroll
+      for (int i = 0; i < WFI; ++i)
+#pragma unroll
+        for (int j = 0; j < WFJ; ++j) accw[i][j] = mfma(av[i], bv[j], accw[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's loads / a-tile DMA
+    buf ^= 1;
+  }
+  // per-block partials: BN-backward sums (part[b][2][C]) and dW (wpart[b][K][C])
+  epi_flush_sums<C, DFI, DWCO, NW>(st_s, st_q, lds, wave, lg, rho, dwco0, b, 0, C, part);
+  float* dst = wpart + static_cast<int64_t>(b) * K * C;
+#pragma unroll
+  for (int i = 0; i < WFI; ++i)
+#pragma unroll
+    for (int j = 0; j < WFJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dst[static_cast<int64_t>(wk0 + 16 * i + 4 * lg + r) * C + wc0 + 16 * j + c16] = accw[i][j][r];
+}
+
 // dW = sum over splits of part[split][n].  A 256-thread block owns 64 float4 columns; its 4 waves
 // each sum every 4th split with 4 independent accumulators (16 loads in flight per wave instead
 // of one dependent chain per column), then the 4 wave sums are combined in LDS in a fixed order
@@ -1729,6 +1928,43 @@ int damd_wgrad3x3_launch(const void* x, const void* dy, float* part, void* dw, i
     hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
   else
     hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
+  DAMD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+
+// ---- fused 1x1 backward (K = 256 -> C = 64)
+extern "C" {
+
+int damd_conv1x1_bwd_fused_supported(int K, int C) { return K == 256 && C == 64; }
+
+int damd_conv1x1_bwd_fused_blocks(int64_t M) {
+  const int64_t tiles = (M + 63) / 64;
+  return static_cast<int>(tiles < 256 ? tiles : 256);
+}
+
+// dz, y: [M][K]; coef: [3][K]; wt: [C][K] (the conv weight transposed); a, yb: [M][C]; bnp: [3][C]
+// (mean, scale, shift of the BN on yb); dzo: [M][C]; part: [G][2][C]; wpart: [G][K][C]; dw: [K][C]
+int damd_conv1x1_bwd_fused_launch(const void* dz, const void* y, const float* coef, const void* wt, const void* a,
+                                  const void* yb, const float* bnp, int64_t M, void* dzo, float* part, float* wpart,
+                                  void* dw, int w_dtype, int K, int C, hipStream_t st) {
+  if (!damd_conv1x1_bwd_fused_supported(K, C) || M <= 0 || M >= (int64_t{1} << 31) - 4096) return -1;
+  const int G = damd_conv1x1_bwd_fused_blocks(M);
+  constexpr int kK = 256, kC = 64;
+  const int lds = ((kK / 64) * 4096 * 3 + 2 * 4096) * 2 + (3 * kK + 3 * kC) * 4;
+  auto* kfn = conv1x1_bwd_fused_kernel<kK, kC>;
+  hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kfn, dim3(G), dim3(512), lds, st, static_cast<const bf16_t*>(dz), static_cast<const bf16_t*>(y),
+                     coef, static_cast<const bf16_t*>(wt), static_cast<const bf16_t*>(a), static_cast<const bf16_t*>(yb),
+                     bnp, static_cast<int>(M), static_cast<bf16_t*>(dzo), part, wpart);
+  const int64_t n = static_cast<int64_t>(K) * C;
+  const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, wpart, G, n, static_cast<bf16_t*>(dw));
+  else
+    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, wpart, G, n, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
   return 0;
 }

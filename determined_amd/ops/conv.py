@@ -434,6 +434,26 @@ class _BNActConvFn(torch.autograd.Function):
         pro_cfgs = ([c for c in range(e.conv_num_cfgs())
                      if e.conv_pro_supported(parked.dz, wt, c) and _allowed("dgrad_bn_pro", c)]
                     if parked is not None and fused else [])
+        fused_bwd = None  # (dz, part, dw) from the one-pass 1x1 backward
+        if (parked is not None and pro_cfgs and k == 1 and not has_res and mask is None and g_a is None
+                and ctx.needs_input_grad[9] and e.conv1x1_bwd_fused_supported(conv_w)
+                and _allowed("bwd1x1_fused", 0)):
+            dzn, yn, coef = parked.dz, parked.y, parked.coef
+            fused_fn = (lambda: e.conv1x1_bwd_fused(dzn, yn, coef, conv_w, a, y, stats))
+
+            def t_fused() -> float:
+                return _time_once(fused_fn)
+
+            def t_plain() -> float:
+                t_d = min(_time_once(lambda c=c: e.conv_dgrad_bn(dzn, wt, 0, c, None, y, None, stats, yn, coef))
+                          for c in pro_cfgs)
+                gz = e.conv_dgrad_bn(dzn, wt, 0, pro_cfgs[-1], None, y, None, stats, yn, coef)[2]
+                return t_d + _time_once(lambda: _wgrad(gz, a, conv_w, 1, 0))
+
+            key = ("bwd1x1_fused_pays", tuple(dzn.shape), tuple(conv_w.shape))
+            if _prologue_pays(key, t_fused, t_plain):
+                fused_bwd = fused_fn()
+                parked = None
         if parked is not None and pro_cfgs and k != 1:
             dzn, yn, coef = parked.dz, parked.y, parked.coef
             plain_cfgs = _igemm_cfgs(e, dzn, wt, 1, k - 1 - pad)
@@ -453,11 +473,13 @@ class _BNActConvFn(torch.autograd.Function):
                 pro_cfgs = []
         if parked is not None and not pro_cfgs:
             g_z, parked = parked.materialise(), None
-        if parked is None:
+        if parked is None and fused_bwd is None:
             g_z = g_z.contiguous(memory_format=cl)
             fused = fused and bool(e.conv_supported(g_z, wt, -1, 1, k - 1 - pad))
         if fused:
-            if parked is not None:  # BN-backward apply of the next BN inside this dgrad's staging
+            if fused_bwd is not None:  # dX (+ BN-backward epilogue) and dW in one pass
+                dz, part, _ = fused_bwd
+            elif parked is not None:  # BN-backward apply of the next BN inside this dgrad's staging
                 dzn, yn, coef = parked.dz, parked.y, parked.coef
                 cands = {c: (lambda c=c: e.conv_dgrad_bn(dzn, wt, k - 1 - pad, c, g_a, y, mask, stats, yn, coef))
                          for c in pro_cfgs}
@@ -479,7 +501,10 @@ class _BNActConvFn(torch.autograd.Function):
             if g_a is not None and mask is None:
                 da, g_a = da + g_a, None
             dy, dg, db, dres = e.bn_act_bwd(da, y, residual, stats, bn_w, True, has_res, mask, g_a)
-        dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
+        if fused_bwd is not None:
+            dw = fused_bwd[2]
+        else:
+            dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
         return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None, None)
 
 

@@ -603,3 +603,35 @@ def test_conv3x3_halo_prologues(ops, shape):
         torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(part, part_ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,hw", [(3, 21), (2, 56)])
+def test_conv1x1_bwd_fused_matches_reference(ops, n, hw):
+    """One-pass 1x1 backward (dy formed from a deferred BN backward, input gradient with the
+    BN-backward epilogue, weight gradient accumulated in the same pass) vs fp32 references."""
+    e = ops.ext()
+    torch.manual_seed(6)
+    cl = torch.channels_last
+    K, C = 256, 64
+    yb = torch.randn(n, C, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    a, stats, _ = e.bn_act_fwd(yb, torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2,
+                               None, None, 0.0, 1e-5, None, True, False, None)
+    w = (torch.randn(K, C, 1, 1, device="cuda") / C ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    dzn = torch.randn(n, K, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yn = torch.randn_like(dzn)
+    coef = torch.randn(3, K, device="cuda").contiguous()
+    assert e.conv1x1_bwd_fused_supported(w)
+    dz, part, dw = e.conv1x1_bwd_fused(dzn, yn, coef, w, a, yb, stats)
+    dy = e.bn_bwd_apply_coef(dzn, yn, coef).float()
+    keep = (yb.float() * stats[2].view(1, -1, 1, 1) + stats[3].view(1, -1, 1, 1)) > 0
+    dz_ref = torch.nn.grad.conv2d_input(yb.shape, w.float(), dy) * keep
+    torch.testing.assert_close(dz.float(), dz_ref, rtol=2e-2, atol=2e-2 * dz_ref.abs().max().item())
+    dzf = dz.float()
+    torch.testing.assert_close(part[:, 0].sum(0), dzf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    cen = yb.float() - stats[0].view(1, -1, 1, 1)
+    torch.testing.assert_close(part[:, 1].sum(0), (dzf * cen).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    dw_ref = torch.nn.grad.conv2d_weight(a.float(), w.shape, dy)
+    assert dw.shape == w.shape and dw.dtype == w.dtype
+    torch.testing.assert_close(dw.float(), dw_ref, rtol=2e-2, atol=2e-2 * dw_ref.abs().max().item())
+    dz2, part2, dw2 = e.conv1x1_bwd_fused(dzn, yn, coef, w, a, yb, stats)
+    assert torch.equal(dz2, dz) and torch.equal(part2, part) and torch.equal(dw2, dw)
