@@ -110,7 +110,7 @@ def test_pid_server_signals_launcher_on_worker_failure(tmp_path):
 def test_pid_server_clean_run(tmp_path):
     sock = str(tmp_path / "p.sock")
     server = subprocess.Popen([sys.executable, "-m", "determined_amd.exec.pid_server", sock, "1", "--",
-                               sys.executable, "-c", "import time; time.sleep(1.0)"], env=ENV)
+                               sys.executable, "-c", "import time; time.sleep(5.0)"], env=ENV)
     while not os.path.exists(sock):
         time.sleep(0.05)
     w = subprocess.run([sys.executable, "-m", "determined_amd.exec.pid_client", sock, "--",
