@@ -79,7 +79,7 @@ extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, i
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
                                     const float*, const float*, const float*, int, const void*, const float*,
-                                    const float*, const float*, void*, uint8_t*, float*, int*);
+                                    const float*, const float*, void*, uint8_t*, float*, int*, int);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
 extern "C" int damd_conv_pro_supported_w(int, int, int, int, int, int, int, int);
 extern "C" int64_t damd_conv_sk_ws_floats(int, int, int);
@@ -809,7 +809,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr, nullptr, sk.wsp, sk.flags);
+                                      nullptr, nullptr, nullptr, sk.wsp, sk.flags, 0);
   TORCH_CHECK(rc == 0, "conv_fwd: launch rejected");
   return {y, part};
 }
@@ -851,7 +851,7 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), 1,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
                                       stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), nullptr, a.data_ptr(),
-                                      want_mask ? mask.data_ptr<uint8_t>() : nullptr, sk.wsp, sk.flags);
+                                      want_mask ? mask.data_ptr<uint8_t>() : nullptr, sk.wsp, sk.flags, 0);
   TORCH_CHECK(rc == 0, "conv_bnact_fwd: launch rejected");
   return {z, part, a, mask};
 }
@@ -885,10 +885,17 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(0) == 4 && stats.size(1) == K &&
               stats.is_contiguous(), "conv_dgrad_bn: stats must be float32 [4, K]");
   const void* d2p = nullptr;
+  int d2hw = 0;
   if (d2.has_value() && d2->defined()) {
-    TORCH_CHECK(d2->sizes() == yb.sizes() && d2->strides() == yb.strides() && d2->scalar_type() == at::kBFloat16,
-                "conv_dgrad_bn: d2 must match yb");
+    // d2 on yb's grid, or the compact [N, K, ceil(H/2), ceil(W/2)] input gradient of a 1x1 stride-2
+    // shortcut conv (nonzero only at the even (h, w) of yb's grid; ops/conv.py _StridedGrad)
+    const bool compact = d2->dim() == 4 && d2->size(0) == N && d2->size(1) == K && d2->size(2) == (H + 1) / 2 &&
+                         d2->size(3) == (W + 1) / 2 && d2->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                         (H > 1 || W > 1);
+    TORCH_CHECK(((d2->sizes() == yb.sizes() && d2->strides() == yb.strides()) || compact) &&
+                d2->scalar_type() == at::kBFloat16, "conv_dgrad_bn: d2 must match yb (or be its stride-2 compact grid)");
     d2p = d2->data_ptr();
+    if (d2->sizes() != yb.sizes()) d2hw = static_cast<int>(((H + 1) / 2) << 16 | ((W + 1) / 2));
   }
   const uint8_t* mp = nullptr;
   if (mask.has_value() && mask->defined() && mask->numel() > 0) {
@@ -936,7 +943,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
                                       yb.data_ptr(), mp, stats[0].data_ptr<float>(), stats[2].data_ptr<float>(),
                                       stats[3].data_ptr<float>(), pro, p_res, p_a, p_c, p_b, p_out, nullptr, sk.wsp,
-                                      sk.flags);
+                                      sk.flags, d2hw);
   TORCH_CHECK(rc == 0, "conv_dgrad_bn: launch rejected");
   if (pro) return {dz, part, dyo};
   return {dz, part};

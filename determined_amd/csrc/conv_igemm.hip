@@ -101,6 +101,8 @@ struct EpiArgs {
   const float* mean;     // BN batch mean [K]
   const float* scale;    // folded BN scale / shift [K] (kEpiBnbR)
   const float* shift;
+  int d2h, d2w;          // 0, 0: d2 is on the output grid; else d2 is the compact (d2h x d2w) gradient of
+                         // a 1x1 stride-2 shortcut's input: nonzero only at even (h, w) of the output grid
 };
 
 // Tile epilogue shared by the conv kernels (EPI modes above): stores the BP x BCO output tile of
@@ -140,16 +142,28 @@ __device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t 
   for (int j0 = 0; j0 < FJ; j0 += JH) {
     bf16x8 dv[JH][FI / 2], yr[JH][FI / 2];
     uint32_t mb[JH][FI / 2];
+    float d2k[JH];
     if (EPI >= kEpiBnbM) {
 #pragma unroll
       for (int jj = 0; jj < JH; ++jj) {
         const int64_t m = pt * BP + wp0 + 16 * (j0 + jj) + rho;
         const int64_t ms = m < g.M ? m : 0;
+        int64_t m2 = ms;  // d2's pixel
+        d2k[jj] = d2f;
+        if (ea.d2h > 0) {  // compact stride-2 grid: odd rows / columns of the output get no d2
+          const uint32_t u = static_cast<uint32_t>(ms), t = u / static_cast<uint32_t>(g.OW);
+          const uint32_t w = u - t * static_cast<uint32_t>(g.OW), n = t / static_cast<uint32_t>(g.OH);
+          const uint32_t h = t - n * static_cast<uint32_t>(g.OH);
+          const bool on = ((h | w) & 1u) == 0;
+          m2 = on ? (static_cast<int64_t>(n) * ea.d2h + (h >> 1)) * ea.d2w + (w >> 1) : 0;
+          d2k[jj] = on ? d2f : 0.f;
+        }
 #pragma unroll
         for (int q = 0; q < FI / 2; ++q) {
-          const int64_t off = ms * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+          const int64_t cof = static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+          const int64_t off = ms * g.K + cof;
           yr[jj][q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
-          dv[jj][q] = *reinterpret_cast<const bf16x8*>(d2p + off);
+          dv[jj][q] = *reinterpret_cast<const bf16x8*>(d2p + m2 * g.K + cof);
           if (EPI == kEpiBnbM) mb[jj][q] = ea.mask[off >> 3];
         }
       }
@@ -171,7 +185,7 @@ __device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t 
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             yv[e] = bf2f(yr[jj][q].v[e]);
-            o[e] += d2f * bf2f(dv[jj][q].v[e]);
+            o[e] += d2k[jj] * bf2f(dv[jj][q].v[e]);
           }
           if (EPI == kEpiBnbM) {
 #pragma unroll
@@ -779,6 +793,9 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
       pprm[g.C + t] = pa.shift[t];
       pprm[2 * g.C + t] = PRO == 2 ? pa.rscale[t] : 0.f;
     }
+    // the first flush() (item 0's halo, before the main loop's first barrier) reads channels
+    // staged by other waves (threads t < C: with C = 64 wave 0 alone writes every parameter)
+    __syncthreads();
   }
   const int prow = lane >> 3, slot = lane & 7;
   const bf16_t* wsrc[NIW];
@@ -1652,7 +1669,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
                          const float* scale, const float* shift, int pro, const void* p_res, const float* p_scale,
                          const float* p_shift, const float* p_rscale, void* p_aout, uint8_t* p_mout, float* sk_ws,
-                         int* sk_flags) {
+                         int* sk_flags, int d2hw) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
   if (pro < 0 || pro > 2) return -4;
   if (pro && (!damd_conv_pro_supported_w(C, K, R, S, stride, pad, W, cfg) || p_scale == nullptr || p_shift == nullptr ||
@@ -1676,7 +1693,9 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   g.groups = groups;
   if (c.sk && (sk_ws == nullptr || sk_flags == nullptr || groups != damd_conv_groups(g.M, K, W, cfg, 0))) return -5;
   const SkArgs ska{sk_ws, sk_flags, sk_flags + kSkMaxBlocks};
-  EpiArgs ea{static_cast<const bf16_t*>(d2), static_cast<const bf16_t*>(yb), mask, mean, scale, shift};
+  EpiArgs ea{static_cast<const bf16_t*>(d2), static_cast<const bf16_t*>(yb), mask, mean, scale, shift, d2hw >> 16,
+             d2hw & 0xffff};
+  if (d2hw != 0 && (d2 == nullptr || epi < 2 || ea.d2h != (g.OH + 1) / 2 || ea.d2w != (g.OW + 1) / 2)) return -3;
   const dim3 grid(static_cast<unsigned>(g.ctiles * groups));
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);

@@ -277,17 +277,60 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
     return cands[_pick(key, cands, default="miopen")]()
 
 
-class _IGemmConvFn(torch.autograd.Function):
-    """Forward on conv_igemm.hip (+ BN statistic partials); backward: input gradient by
-    :func:`_dgrad`, weight gradient on MIOpen."""
+class _StridedGrad:
+    """The input gradient of a 1x1 stride-2 shortcut conv kept on its compact grid.
+
+    A stride-2 1x1 conv reads only the even (h, w) pixels of its input, so its input gradient is
+    zero elsewhere: dX[:, :, ::2, ::2] = dY x W^T, a plain stride-1 1x1 input gradient on the
+    output grid.  Materialising it at full resolution (MIOpen's strided backward-data + a zero
+    fill, then a full-size read by the consumer) moves 4x the bytes.  When the conv's input is
+    the ``a`` output of a :class:`_BNActConvFn` node (its only consumer: ``models/resnet.py
+    _chain_blocks`` stage transitions), the conv's node returns an unwritten placeholder of the
+    input's shape and parks the compact gradient here; that node's backward takes it and adds it
+    inside its input-gradient epilogue at the even pixels only (conv_igemm.hip ``EpiArgs.d2h``),
+    or materialises it when it cannot fuse."""
+
+    _pending: Dict[int, "_StridedGrad"] = {}
+
+    def __init__(self, placeholder: torch.Tensor, compact: torch.Tensor):
+        self.placeholder, self.compact = placeholder, compact
+
+    @classmethod
+    def park(cls, x: torch.Tensor, compact: torch.Tensor) -> torch.Tensor:
+        ph = torch.empty_like(x, memory_format=torch.channels_last)
+        cls._pending[ph.data_ptr()] = cls(ph, compact)
+        return ph
+
+    @classmethod
+    def take(cls, g: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        if g is None:
+            return None
+        ent = cls._pending.get(g.data_ptr())
+        if ent is None or ent.placeholder.shape != g.shape or ent.placeholder.stride() != g.stride():
+            return None
+        del cls._pending[g.data_ptr()]
+        return ent.compact
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, want_stats, cfg):
+    def materialise(compact: torch.Tensor, shape) -> torch.Tensor:
+        full = torch.zeros(shape, device=compact.device, dtype=compact.dtype).contiguous(
+            memory_format=torch.channels_last)
+        full[:, :, ::2, ::2] = compact
+        return full
+
+
+class _IGemmConvFn(torch.autograd.Function):
+    """Forward on conv_igemm.hip (+ BN statistic partials); backward: input gradient by
+    :func:`_dgrad`, weight gradient by :func:`_wgrad`.  ``compact_dx``: a 1x1 stride-2 conv whose
+    input gradient goes to a :class:`_BNActConvFn` node on the compact grid (:class:`_StridedGrad`)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, want_stats, cfg, compact_dx=False):
         from determined_amd import ops
 
         y, part = ops.ext().conv_fwd(x, weight, stride, pad, want_stats, cfg, 0)
         ctx.save_for_backward(x, weight)
-        ctx.geo = (stride, pad)
+        ctx.geo = (stride, pad, bool(compact_dx))
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         return y, part
@@ -295,14 +338,19 @@ class _IGemmConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dpart=None):
         x, weight = ctx.saved_tensors
-        stride, pad = ctx.geo
+        stride, pad, compact = ctx.geo
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, weight, stride, pad)
+            if compact:  # dX on the output grid: the stride-1 1x1 input gradient of dY
+                xc = torch.empty((x.shape[0], x.shape[1]) + tuple(dy.shape[2:]), device=x.device, dtype=x.dtype,
+                                 memory_format=torch.channels_last)  # shape only (MIOpen candidate)
+                dx = _StridedGrad.park(x, _dgrad(dy, xc, weight, 1, 0).contiguous(memory_format=torch.channels_last))
+            else:
+                dx = _dgrad(dy, x, weight, stride, pad)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy, x, weight, stride, pad)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def igemm_fusable(conv: nn.Module, x: torch.Tensor) -> bool:
@@ -317,6 +365,15 @@ def igemm_fusable(conv: nn.Module, x: torch.Tensor) -> bool:
 
     return ops.fusion_enabled("igemm_conv") and bool(ops.ext().conv_supported(x, conv.weight, -1, conv.stride[0],
                                                                               conv.padding[0]))
+
+
+def _compact_dx_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """A 1x1 stride-2 conv whose input is the ``a`` output of a :class:`_BNActConvFn` node: its
+    input gradient can stay on the compact grid (:class:`_StridedGrad`)."""
+    from determined_amd import ops
+
+    return (conv.kernel_size == (1, 1) and conv.stride == (2, 2) and conv.padding == (0, 0) and x.requires_grad
+            and isinstance(x.grad_fn, _BNActConvFn._backward_cls) and ops.fusion_enabled("compact_shortcut_grad"))
 
 
 def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -335,7 +392,7 @@ def conv_bn_input(conv: nn.Conv2d, x: torch.Tensor, stats: bool = True) -> Tuple
     cands = {c: (lambda c=c: e.conv_fwd(x, w, st, pad, True, c, 0)) for c in _igemm_cfgs(e, x, w, st, pad)}
     cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
     stats = stats and ops.fusion_enabled("conv_stats")
-    y, part = _IGemmConvFn.apply(x, w, st, pad, stats, cfg)
+    y, part = _IGemmConvFn.apply(x, w, st, pad, stats, cfg, _compact_dx_ok(conv, x))
     return y, (part if stats else None)
 
 
@@ -427,6 +484,9 @@ class _BNActConvFn(torch.autograd.Function):
         k = conv_w.shape[2]
         if g_z is None:  # the conv output is always consumed in the networks this node serves
             raise RuntimeError("bn_act_conv: the conv output received no gradient")
+        g_ac = _StridedGrad.take(g_a)  # a stride-2 shortcut's input gradient on its compact grid
+        if g_ac is not None:
+            g_a = g_ac
         g_a = None if g_a is None else g_a.contiguous(memory_format=cl)
         parked = _LazyBNGrad.take(g_z)  # g_z may be a deferred BN backward (the next BN's node)
         wt = _flip_weight(conv_w) if stride == 1 and 2 * pad == k - 1 else None
@@ -468,7 +528,8 @@ class _BNActConvFn(torch.autograd.Function):
                     _time_once(lambda c=c: e.conv_dgrad_bn(gz, wt, k - 1 - pad, c, g_a, y, mask, stats, None, None))
                     for c in plain_cfgs)
 
-            key = ("dgrad_pro_pays", tuple(dzn.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+            key = ("dgrad_pro_pays", tuple(dzn.shape), tuple(conv_w.shape), mask is not None,
+                   None if g_a is None else tuple(g_a.shape))
             if not plain_cfgs or not _prologue_pays(key, t_fused, t_plain):
                 pro_cfgs = []
         if parked is not None and not pro_cfgs:
@@ -476,6 +537,8 @@ class _BNActConvFn(torch.autograd.Function):
         if parked is None and fused_bwd is None:
             g_z = g_z.contiguous(memory_format=cl)
             fused = fused and bool(e.conv_supported(g_z, wt, -1, 1, k - 1 - pad))
+        if g_ac is not None and not fused:  # the unfused composition needs it at full size
+            g_a = _StridedGrad.materialise(g_a, y.shape)
         if fused:
             if fused_bwd is not None:  # dX (+ BN-backward epilogue) and dW in one pass
                 dz, part, _ = fused_bwd
@@ -483,12 +546,14 @@ class _BNActConvFn(torch.autograd.Function):
                 dzn, yn, coef = parked.dz, parked.y, parked.coef
                 cands = {c: (lambda c=c: e.conv_dgrad_bn(dzn, wt, k - 1 - pad, c, g_a, y, mask, stats, yn, coef))
                          for c in pro_cfgs}
-                key = ("dgrad_bn_pro", tuple(dzn.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+                key = ("dgrad_bn_pro", tuple(dzn.shape), tuple(conv_w.shape), mask is not None,
+                       None if g_a is None else tuple(g_a.shape))
                 dz, part, g_z = cands[_pick(key, cands, default=pro_cfgs[-1])]()
             else:
                 cands = {c: (lambda c=c: e.conv_dgrad_bn(g_z, wt, k - 1 - pad, c, g_a, y, mask, stats, None, None))
                          for c in _igemm_cfgs(e, g_z, wt, 1, k - 1 - pad)}
-                key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None, g_a is not None)
+                key = ("dgrad_bn", tuple(g_z.shape), tuple(conv_w.shape), mask is not None,
+                       None if g_a is None else tuple(g_a.shape))
                 dz, part = cands[_pick(key, cands, default=e.conv_default_cfg(wt.shape[0]))]()
             if lazy:  # defer this BN's apply pass into the conv that produced y
                 coef, dg, db = e.bn_bwd_finalize_part(y, stats, bn_w, part)

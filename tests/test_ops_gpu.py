@@ -443,6 +443,101 @@ def test_conv_dgrad_bn_epilogue(ops, k, masked, with_d2):
         torch.testing.assert_close(part[:, 1].sum(0), (dzf * cen).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("k,hw", [(1, 10), (1, 7), (3, 10)])
+def test_conv_dgrad_bn_compact_d2(ops, k, hw):
+    """conv_dgrad_bn with d2 on the compact stride-2 grid (the input gradient of a 1x1 stride-2
+    shortcut conv, ops/conv.py _StridedGrad) == the same call with d2 materialised at full size."""
+    from determined_amd.ops.conv import _StridedGrad
+
+    e = ops.ext()
+    torch.manual_seed(5)
+    n, cin, cout = 3, 128, 64
+    cl = torch.channels_last
+    w = (torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)
+    g = torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yb = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    res = torch.randn_like(yb)
+    _, stats, mask = e.bn_act_fwd(yb, torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2,
+                                  None, None, 0.0, 1e-5, res, True, True, None)
+    hc = (hw + 1) // 2
+    d2c = torch.randn(n, cin, hc, hc, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    d2f = _StridedGrad.materialise(d2c, yb.shape)
+    assert torch.equal(d2f[:, :, ::2, ::2], d2c) and d2f[:, :, 1::2].abs().sum().item() == 0
+    for cfg in [c for c in range(e.conv_num_cfgs()) if e.conv_supported(g, wt, c, 1, k // 2)]:
+        dz_ref, part_ref = e.conv_dgrad_bn(g, wt, k // 2, cfg, d2f, yb, mask, stats, None, None)
+        dz, part = e.conv_dgrad_bn(g, wt, k // 2, cfg, d2c, yb, mask, stats, None, None)
+        torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=0, atol=0)
+        torch.testing.assert_close(part, part_ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,k,hw,c", [(16, 2048, 3, 1024), (16, 1024, 6, 512), (16, 512, 12, 256), (2, 2048, 7, 1024)])
+def test_conv_1x1_dgrad_every_cfg_small_grids(ops, n, k, hw, c):
+    """The stride-1 1x1 input gradient (conv_fwd of dY with the transposed weights) for every tile
+    config on the small pixel counts of compact shortcut gradients (M = 144 .. 2304) vs fp32."""
+    e = ops.ext()
+    torch.manual_seed(2)
+    cl = torch.channels_last
+    w = (torch.randn(k, c, 1, 1, device="cuda") / k ** 0.5).to(torch.bfloat16)
+    wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=cl)
+    dy = torch.randn(n, k, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    ref = torch.nn.grad.conv2d_input((n, c, hw, hw), w.float(), dy.float())
+    bad = []
+    for cfg in [q for q in range(e.conv_num_cfgs()) if e.conv_supported(dy, wt, q, 1, 0)]:
+        dx = e.conv_fwd(dy, wt, 1, 0, False, cfg, 0)[0].float()
+        err = ((dx - ref).norm() / ref.norm()).item()
+        if not err < 1e-2:
+            bad.append((cfg, err))
+    assert not bad, bad
+
+
+def test_stage_transition_compact_shortcut_grad(ops, monkeypatch):
+    """A chained stage transition (1x1 stride-2 downsample fed by a fused BN->conv node): the
+    shortcut's input gradient stays compact and is added in the consumer's dgrad epilogue; the
+    gradients match the run with that fusion off and an fp32 reference."""
+    import copy
+    from determined_amd.models.resnet import Bottleneck, _chain_blocks
+    from determined_amd.ops.bn import BatchNormAct2d
+    from determined_amd.ops.conv import _StridedGrad
+
+    torch.manual_seed(1)
+    ds1 = torch.nn.Sequential(torch.nn.Conv2d(64, 256, 1, bias=False), BatchNormAct2d(256, act=False))
+    ds2 = torch.nn.Sequential(torch.nn.Conv2d(256, 512, 1, stride=2, bias=False), BatchNormAct2d(512, act=False))
+    blocks = torch.nn.ModuleList([Bottleneck(64, 64, 1, ds1), Bottleneck(256, 128, 2, ds2), Bottleneck(512, 128)])
+    for mod in blocks.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    x0 = torch.randn(8, 64, 16, 16)
+    g0 = torch.randn(8, 512, 8, 8)
+    seen = []
+    orig = _StridedGrad.take.__func__
+
+    def take(cls, g):
+        got = orig(cls, g)
+        seen.append(got is not None)
+        return got
+
+    def run(dtype, disabled):
+        monkeypatch.setattr(ops, "_DISABLED", frozenset(disabled))
+        bl = copy.deepcopy(blocks).cuda().to(dtype).to(memory_format=torch.channels_last)
+        x = x0.cuda().to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        y = _chain_blocks(list(bl), x, False)
+        y.backward(g0.cuda().to(dtype).contiguous(memory_format=torch.channels_last))
+        grads = {n: p.grad.float().cpu() for n, p in bl.named_parameters()}
+        grads["x"] = x.grad.float().cpu()
+        return grads
+
+    monkeypatch.setattr(_StridedGrad, "take", classmethod(take))
+    ref = run(torch.float32, {"bn_conv"})
+    on = run(torch.bfloat16, ())
+    assert any(seen) and not _StridedGrad._pending  # the compact gradient was parked and taken
+    off = run(torch.bfloat16, {"compact_shortcut_grad"})
+    for n, r in ref.items():
+        e_on = ((on[n] - r).norm() / r.norm()).item()
+        e_off = ((off[n] - r).norm() / r.norm()).item()
+        assert e_on < max(1.5 * e_off, 2e-2), (n, e_on, e_off)
+
+
 @pytest.mark.parametrize("depth", [3])
 def test_chained_bottlenecks_match_unchained(ops, monkeypatch, depth):
     """ResNet block chain with every BN fused into its consumer conv's autograd node (ops/conv.py
@@ -603,6 +698,9 @@ def test_conv3x3_halo_prologues(ops, shape):
         torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(part, part_ref, rtol=1e-3, atol=1e-2)
+        for _ in range(12):  # run-to-run identical (a missing barrier before the first halo
+            dz2, _, dy2 = e.conv_dgrad_bn(dzn, wt, 1, cfg, None, yb, None, stb, yn, coef)  # was a race)
+            assert torch.equal(dz2, dz) and torch.equal(dy2, dy)
 
 
 @pytest.mark.parametrize("n,hw", [(3, 21), (2, 56)])
