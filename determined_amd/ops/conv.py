@@ -220,7 +220,10 @@ def _igemm_cfgs(ext, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int):
 
 def _flip_weight(w: torch.Tensor) -> torch.Tensor:
     """[K, C, R, S] -> [C, K, R, S] rotated by 180 degrees: the stride-1 input gradient is the
-    forward convolution of dY with these weights (padding R - 1 - pad)."""
+    forward convolution of dY with these weights (padding R - 1 - pad).  1x1: the transpose alone
+    (one copy kernel instead of a flip kernel + a copy per backward)."""
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
 
 
