@@ -638,6 +638,7 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
     pre = stats_part->data_ptr<float>();
     pre_nb = static_cast<int>(stats_part->size(0));
   }
+  TORCH_CHECK(N * OH * OW * C < (int64_t{1} << 31), "bn_pool_fwd: pooled tensor too large (32-bit indexing)");
   damd_bn_pool_fwd_launch(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, static_cast<int>(H), static_cast<int>(W),
                           static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW), weight.data_ptr(),
                           bias.data_ptr(), rm, rv, static_cast<float>(momentum), static_cast<float>(eps),
@@ -678,6 +679,7 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dp, const at::Tensor& idx,
                 "bn_pool_bwd: xarg must match dp");
     xa = xarg->data_ptr();
   }
+  TORCH_CHECK(N * OH * OW * C < (int64_t{1} << 31), "bn_pool_bwd: pooled tensor too large (32-bit indexing)");
   damd_bn_pool_bwd_launch(dp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), N, static_cast<int>(H),
                           static_cast<int>(W), static_cast<int>(C), static_cast<int>(OH), static_cast<int>(OW),
                           stats[0].data_ptr<float>(), stats[1].data_ptr<float>(), stats[2].data_ptr<float>(),
@@ -817,8 +819,12 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
 // z = conv1x1(a, w) with a = relu(y * stats[2] + stats[3] [+ res]) computed inside the conv's
 // operand staging (ProArgs); returns (z, z's BN statistic partials [groups, 2, K], a, a's ReLU bit
 // mask or an empty tensor).  stats: [4, C] of y's BatchNorm (mean, invstd, scale, shift).
+// res_stats: [4, C] stats of a BatchNorm (no ReLU) whose output is the residual: `res` is then
+// that BN's INPUT and a = relu(y * scale + shift + res * res_scale + res_shift) (the residual BN's
+// forward apply folded into this staging too).
 std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w, const c10::optional<at::Tensor>& res,
-                                       const at::Tensor& stats, bool want_mask, int64_t cfg) {
+                                       const at::Tensor& stats, bool want_mask, int64_t cfg,
+                                       const c10::optional<at::Tensor>& res_stats) {
   const int64_t R = w.size(2), S = w.size(3), pad = (R - 1) / 2;  // 1x1, or 3x3 / pad 1 (halo kernel)
   TORCH_CHECK(R == S && (R == 1 || R == 3) && conv_supported(y, w, cfg, 1, pad), "conv_bnact_fwd: unsupported input");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3), K = w.size(0);
@@ -836,6 +842,17 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
                 "conv_bnact_fwd: res must match y");
     rp = res->data_ptr();
   }
+  const float* shift = stats[3].data_ptr<float>();
+  const float* rscale = nullptr;
+  at::Tensor shift_comb;
+  if (res_stats.has_value() && res_stats->defined()) {
+    TORCH_CHECK(rp != nullptr && res_stats->scalar_type() == at::kFloat && res_stats->dim() == 2 &&
+                res_stats->size(0) == 4 && res_stats->size(1) == C && res_stats->is_contiguous(),
+                "conv_bnact_fwd: res_stats must be float32 [4, C] with a residual");
+    shift_comb = stats[3] + (*res_stats)[3];
+    shift = shift_comb.data_ptr<float>();
+    rscale = (*res_stats)[2].data_ptr<float>();
+  }
   const int64_t M = N * H * W;
   TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_bnact_fwd: tensor too large");
   auto wl = w.contiguous(at::MemoryFormat::ChannelsLast);
@@ -850,7 +867,7 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), 1,
                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, rp,
-                                      stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), nullptr, a.data_ptr(),
+                                      stats[2].data_ptr<float>(), shift, rscale, a.data_ptr(),
                                       want_mask ? mask.data_ptr<uint8_t>() : nullptr, sk.wsp, sk.flags, 0);
   TORCH_CHECK(rc == 0, "conv_bnact_fwd: launch rejected");
   return {z, part, a, mask};

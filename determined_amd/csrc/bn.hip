@@ -429,6 +429,16 @@ struct PoolGeo {
   int H, W, OH, OW;
 };
 
+// (n, oh, ow) of pooled position q in 32-bit arithmetic (the host checks that the element-vector
+// counts fit in 31 bits): a 64-bit division is a ~100-instruction software routine per call
+__device__ __forceinline__ void pool_pos(uint32_t q, const PoolGeo& g, int64_t& n, int& oh, int& ow) {
+  const uint32_t t = q / static_cast<uint32_t>(g.OW);
+  ow = static_cast<int>(q - t * static_cast<uint32_t>(g.OW));
+  const uint32_t nn = t / static_cast<uint32_t>(g.OH);
+  oh = static_cast<int>(t - nn * static_cast<uint32_t>(g.OH));
+  n = nn;
+}
+
 // window index of input (h, w) inside output window (oh, ow) (kernel 3, stride 2, pad 1)
 __device__ __forceinline__ int win_pos(int h, int w, int oh, int ow) { return (h - 2 * oh + 1) * 3 + (w - 2 * ow + 1); }
 
@@ -445,10 +455,9 @@ bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc
   V8<float>::ld(scale + cg * 8, sc);
   V8<float>::ld(shift + cg * 8, sh);
   for (int64_t v = T0; v < Vout; v += stride) {
-    const int64_t pix = v / TPR;  // (n, oh, ow)
-    const int ow = static_cast<int>(pix % g.OW);
-    const int oh = static_cast<int>((pix / g.OW) % g.OH);
-    const int64_t n = pix / (static_cast<int64_t>(g.OW) * g.OH);
+    int64_t n;
+    int oh, ow;
+    pool_pos(static_cast<uint32_t>(v) / static_cast<uint32_t>(TPR), g, n, oh, ow);
     float best[8], xa[8];
     int arg[8];
 #pragma unroll
@@ -605,9 +614,9 @@ maxpool_bn_bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ dp2
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s[k] = 0.f; sx[k] = 0.f; }
     for (int64_t q = r0 + rsub; q < r1; q += geo_.RS) {
-      const int ow = static_cast<int>(q % g.OW);
-      const int oh = static_cast<int>((q / g.OW) % g.OH);
-      const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
+      int64_t n;
+      int oh, ow;
+      pool_pos(static_cast<uint32_t>(q), g, n, oh, ow);
       float dr[4][8];
       quad_pool_grad(dp, dp2, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll
@@ -663,10 +672,9 @@ maxpool_bn_bwd_apply_kernel(const T* __restrict__ dp, const T* __restrict__ dp2,
   V8<float>::ld(scale + cg * 8, sc);
   V8<float>::ld(shift + cg * 8, sh);
   for (int64_t v = T0; v < VQ; v += stride) {
-    const int64_t q = v / TPR;
-    const int ow = static_cast<int>(q % g.OW);
-    const int oh = static_cast<int>((q / g.OW) % g.OH);
-    const int64_t n = q / (static_cast<int64_t>(g.OW) * g.OH);
+    int64_t n;
+    int oh, ow;
+    pool_pos(static_cast<uint32_t>(v) / static_cast<uint32_t>(TPR), g, n, oh, ow);
     float dr[4][8];
     quad_pool_grad(dp, dp2, idx, n, oh, ow, cg, C, g, dr);
 #pragma unroll

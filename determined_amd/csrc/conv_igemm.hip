@@ -121,7 +121,8 @@ struct ProArgs {
   const bf16_t* res;     // residual added before the ReLU (PRO 1) / BN input y (PRO 2), or null
   const float* scale;    // per input channel [C]: folded BN scale (PRO 1) / A (PRO 2)
   const float* shift;    //                         folded BN shift (PRO 1) / Cc (PRO 2)
-  const float* rscale;   // PRO 2: B (scale of res); PRO 1: unused (res enters with weight 1)
+  const float* rscale;   // PRO 2: B (scale of res); PRO 1: null (res enters with weight 1) or the
+                         // residual's own folded BN scale (its shift is pre-added to `shift`)
   bf16_t* aout;          // the operand, [M][C], or null
   uint8_t* mout;         // PRO 1: ReLU bit mask of a, [M][C/8], or null
 };
@@ -521,7 +522,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     psc[1] = *reinterpret_cast<const float4*>(pa.scale + cofs + 4);
     psh[0] = *reinterpret_cast<const float4*>(pa.shift + cofs);
     psh[1] = *reinterpret_cast<const float4*>(pa.shift + cofs + 4);
-    if (PRO == 2) {
+    if (PRO == 2 || pa.rscale != nullptr) {
       prs[0] = *reinterpret_cast<const float4*>(pa.rscale + cofs);
       prs[1] = *reinterpret_cast<const float4*>(pa.rscale + cofs + 4);
     }
@@ -534,7 +535,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     float rs[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) rs[e] = 1.f;
-    if (PRO == 2) {
+    if (PRO == 2 || pa.rscale != nullptr) {
       rs[0] = prs[0].x; rs[1] = prs[0].y; rs[2] = prs[0].z; rs[3] = prs[0].w;
       rs[4] = prs[1].x; rs[5] = prs[1].y; rs[6] = prs[1].z; rs[7] = prs[1].w;
     }
@@ -546,7 +547,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float t = bf2f(py[i].v[e]) * sc[e] + sh[e];
-        if (has_res) t += (PRO == 2 ? rs[e] : 1.f) * bf2f(pr[i].v[e]);
+        if (has_res) t += rs[e] * bf2f(pr[i].v[e]);
         v[e] = PRO == 1 ? fmaxf(t, 0.f) : t;
       }
       bf16x8 o;

@@ -14,7 +14,7 @@ from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 from determined_amd.ops import fusion_enabled
-from determined_amd.ops.conv import bn_act_conv, conv_bn_input, stem_conv2d
+from determined_amd.ops.conv import LazyBNResidual, _materialise, bn_act_conv, conv_bn_input, stem_conv2d
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -31,13 +31,16 @@ def _chainable(blk: nn.Module) -> bool:
             and not blk._forward_pre_hooks)
 
 
-def _downsample(ds: nn.Module, x: torch.Tensor) -> torch.Tensor:
+def _downsample(ds: nn.Module, x: torch.Tensor, lazy_bn: bool = False):
     """``ds(x)`` for the ``Sequential(conv1x1, BatchNormAct2d)`` shortcut, with the BN statistics
-    from the conv epilogue."""
+    from the conv epilogue.  ``lazy_bn``: return the BN as a :class:`LazyBNResidual` (its apply
+    pass folds into the consumer's conv prologue; ``_chain_blocks``)."""
     if (isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[1], BatchNormAct2d)
             and not ds._forward_hooks and not ds._forward_pre_hooks and not ds[1]._forward_hooks
             and not ds[1]._forward_pre_hooks):
         y, part = conv_bn_input(ds[0], x)
+        if lazy_bn and part is not None and not ds[1].act and ds[1].kernel_path(y):
+            return LazyBNResidual(y, part, ds[1])
         return ds[1](y, stats_part=part)
     return ds(x)
 
@@ -95,13 +98,13 @@ def _chain_blocks(blocks, x, split: bool):
             y_prev, p_prev, res_prev, bn_prev, lazy_prev = pending
             xs, y, part = bn_act_conv(bn_prev, y_prev, p_prev, res_prev, convs[0], lazy_grad=lazy_prev)
             lazy = _pro_conv(convs[0])
-        identity = xs if blk.downsample is None else _downsample(blk.downsample, xs)
+        identity = xs if blk.downsample is None else _downsample(blk.downsample, xs, lazy_bn=True)
         for bn, conv in zip(bns[:-1], convs[1:]):
             _, y, part = bn_act_conv(bn, y, part, None, conv, lazy_grad=lazy)
             lazy = _pro_conv(conv)
         pending = (y, part, identity, bns[-1], lazy)
     y, part, identity, bn, _ = pending
-    return bn(y, identity, stats_part=part)
+    return bn(y, _materialise(identity), stats_part=part)
 
 
 def _pro_conv(conv: nn.Conv2d) -> bool:

@@ -442,6 +442,24 @@ class _LazyBNGrad:
         return ops.ext().bn_bwd_apply_coef(self.dz, self.y, self.coef)
 
 
+class LazyBNResidual:
+    """A shortcut ``r = bn(y)`` (BatchNorm without ReLU, e.g. ResNet's downsample BN) kept as its
+    input ``y`` + the statistic partials of ``y`` from the producing conv.  When the consumer is a
+    :func:`bn_act_conv` whose conv stages its operand through the BN prologue, ``r``'s apply pass
+    folds into that staging (a = relu(bn(x) + y * r_scale + r_shift); conv_igemm.hip ProArgs
+    ``rscale``) and ``r`` is never written; any other consumer calls :meth:`materialise`."""
+
+    def __init__(self, y: torch.Tensor, part: Optional[torch.Tensor], bn: nn.Module):
+        self.y, self.part, self.bn = y, part, bn
+
+    def materialise(self) -> torch.Tensor:
+        return self.bn(self.y, stats_part=self.part)
+
+
+def _materialise(r):
+    return r.materialise() if isinstance(r, LazyBNResidual) else r
+
+
 class _BNActConvFn(torch.autograd.Function):
     """``a = relu(bn(y) [+ residual])``, ``z = conv(a)`` (+ the BN statistic partials of z) as one
     autograd node (the forward apply inside the conv's operand staging where a prologue config
@@ -454,21 +472,28 @@ class _BNActConvFn(torch.autograd.Function):
     (strided conv, config unsupported) the backward is the unfused composition."""
 
     @staticmethod
-    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg, pro, lazy):
+    def forward(ctx, y, bn_w, bn_b, rm, rv, residual, momentum, eps, stats_part, conv_w, stride, pad, cfg, pro, lazy,
+                res_w=None, res_b=None, res_args=None):
         from determined_amd import ops
 
         e = ops.ext()
+        rstats = None
+        if res_w is not None:  # residual = bn_r(residual) folded into the prologue (LazyBNResidual)
+            r_rm, r_rv, r_mom, r_eps, r_part = res_args
+            rstats = e.bn_finalize_part(r_part, residual.numel() // residual.shape[1], res_w, res_b, r_rm, r_rv,
+                                        float(r_mom), float(r_eps))
         if pro:  # 1x1 conv applies the BN(+residual)+ReLU while staging its input (conv_igemm.hip PRO)
             stats = e.bn_finalize_part(stats_part, y.numel() // y.shape[1], bn_w, bn_b, rm, rv, float(momentum),
                                        float(eps))
-            z, part, a, mask = e.conv_bnact_fwd(y, conv_w, residual, stats, residual is not None, cfg)
+            z, part, a, mask = e.conv_bnact_fwd(y, conv_w, residual, stats, residual is not None, cfg, rstats)
         else:
             a, stats, mask = e.bn_act_fwd(y, bn_w, bn_b, rm, rv, float(momentum), float(eps), residual, True, True,
                                           stats_part)
             z, part = e.conv_fwd(a, conv_w, stride, pad, True, cfg, 0)
         masked = mask.numel() > 0
         ctx.save_for_backward(y, stats, bn_w, mask if masked else None, a, conv_w,
-                              residual if (residual is not None and not masked) else None)
+                              residual if (residual is not None and (not masked or rstats is not None)) else None,
+                              rstats, res_w)
         ctx.geo = (stride, pad, residual is not None, bool(lazy))
         ctx.mark_non_differentiable(part)
         # an unused `a` (BN1/BN2 outputs have no second consumer) must arrive as None, not as a
@@ -481,8 +506,10 @@ class _BNActConvFn(torch.autograd.Function):
         from determined_amd import ops
 
         e = ops.ext()
-        y, stats, bn_w, mask, a, conv_w, residual = ctx.saved_tensors
+        y, stats, bn_w, mask, a, conv_w, residual, rstats, res_w = ctx.saved_tensors
         stride, pad, has_res, lazy = ctx.geo
+        if rstats is not None:  # the folded residual BN's input is saved, not the residual itself
+            res_in, residual = residual, None
         cl = torch.channels_last
         k = conv_w.shape[2]
         if g_z is None:  # the conv output is always consumed in the networks this node serves
@@ -573,7 +600,12 @@ class _BNActConvFn(torch.autograd.Function):
             dw = fused_bwd[2]
         else:
             dw = _wgrad(g_z, a, conv_w, stride, pad) if ctx.needs_input_grad[9] else None
-        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None, None)
+        dg_r = db_r = None
+        if rstats is not None and dres is not None:  # backward of the folded residual BN (no ReLU)
+            dres = dres.contiguous(memory_format=cl)
+            dres, dg_r, db_r, _ = e.bn_act_bwd(dres, res_in, None, rstats, res_w, False, False, None, None)
+        return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None, None,
+                dg_r, db_r, None)
 
 
 def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tensor], residual: Optional[torch.Tensor],
@@ -587,8 +619,14 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
     from determined_amd import ops
     from determined_amd.ops.bn import BatchNormAct2d
 
+    lres = residual if isinstance(residual, LazyBNResidual) else None
+    if lres is not None and not (isinstance(lres.bn, BatchNormAct2d) and not lres.bn.act and _plain_module(lres.bn)
+                                 and lres.part is not None and lres.bn.kernel_path(lres.y)
+                                 and ops.fusion_enabled("bn_residual_fold")):
+        residual, lres = lres.materialise(), None
+    rt = lres.y if lres is not None else residual  # the residual operand tensor
     if (isinstance(bn, BatchNormAct2d) and bn.act and _plain_module(bn) and ops.fusion_enabled("bn_conv")
-            and igemm_fusable(conv, y) and bn.kernel_path(y, residual) and y.shape[1] == conv.in_channels):
+            and igemm_fusable(conv, y) and bn.kernel_path(y, rt) and y.shape[1] == conv.in_channels):
         e = ops.ext()
         rm, rv, momentum = bn.train_step_args()
         st, pad = conv.stride[0], conv.padding[0]
@@ -603,7 +641,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
             dummy[2].fill_(1.0)
 
             def t_fused() -> float:
-                return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, None, dummy, False, c)) for c in pro_cfgs)
+                return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, None, dummy, False, c, None)) for c in pro_cfgs)
 
             def t_plain() -> float:
                 apply = (lambda: e.bn_act_fwd(y, bn.weight, bn.bias, None, None, 0.0, float(bn.eps), None, True, True,
@@ -614,15 +652,23 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
 
             if not _prologue_pays(("fwd_pro_pays", tuple(y.shape), tuple(w.shape)), t_fused, t_plain):
                 pro_cfgs = []
+        if lres is not None and not (pro_cfgs and w.shape[2] == 1):  # no 1x1 prologue to fold it into
+            residual, lres = lres.materialise(), None
+            rt = residual
         if pro_cfgs:  # the BN apply pass moves into the conv's operand staging
-            key = ("fwd_pro", tuple(y.shape), tuple(w.shape), residual is not None)
+            key = ("fwd_pro", tuple(y.shape), tuple(w.shape), rt is not None)
             cfg = _TUNE.get(key)
             if cfg not in pro_cfgs:  # tune on stand-in BN parameters (timing does not depend on them)
                 dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
                 dummy[2].fill_(1.0)
-                cands = {c: (lambda c=c: e.conv_bnact_fwd(y, w, residual, dummy, residual is not None, c))
+                cands = {c: (lambda c=c: e.conv_bnact_fwd(y, w, rt, dummy, rt is not None, c, None))
                          for c in pro_cfgs}
                 cfg = _pick(key, cands, default=pro_cfgs[-1])
+            if lres is not None:  # the residual's own BN apply folds into the same staging
+                r_rm, r_rv, r_mom = lres.bn.train_step_args()
+                return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, rt, momentum, bn.eps, stats_part, w, st,
+                                          pad, cfg, True, lazy, lres.bn.weight, lres.bn.bias,
+                                          (r_rm, r_rv, r_mom, lres.bn.eps, lres.part))
             return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st,
                                       pad, cfg, True, lazy)
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)
@@ -632,6 +678,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
             cfg = _pick(key, cands, default=e.conv_default_cfg(w.shape[0]))
         return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st, pad,
                                   cfg, False, lazy)
+    residual = _materialise(residual)
     a = bn(y, residual, stats_part=stats_part)
     z, part = conv_bn_input(conv, a)
     return a, z, part

@@ -221,7 +221,7 @@ def test_resnet50_bf16_fused_gradients_match_unfused(bnmod, monkeypatch):
     from determined_amd.models.resnet import resnet50
 
     all_fusions = frozenset({"stem_conv", "stem_stats", "split_grad", "avgpool", "igemm_conv", "conv_stats",
-                             "bn_conv", "bn_prologue", "bn_lazy_bwd", "compact_shortcut_grad"})
+                             "bn_conv", "bn_prologue", "bn_lazy_bwd", "compact_shortcut_grad", "bn_residual_fold"})
     torch.manual_seed(0)
     model = resnet50(num_classes=10, zero_init_residual=False).cuda().to(memory_format=torch.channels_last)
     state = {k: v.clone() for k, v in model.state_dict().items()}

@@ -601,7 +601,7 @@ def test_conv_bnact_prologue_matches_composition(ops, with_res):
     cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
     assert cfgs
     for cfg in cfgs:
-        z, part, a, mask = e.conv_bnact_fwd(y, w, res, stats, with_res, cfg)
+        z, part, a, mask = e.conv_bnact_fwd(y, w, res, stats, with_res, cfg, None)
         torch.testing.assert_close(a, a_ref, rtol=0, atol=0)
         if with_res:
             assert torch.equal(mask, mask_ref)
@@ -610,6 +610,35 @@ def test_conv_bnact_prologue_matches_composition(ops, with_res):
         torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())
         tol = 2e-3 * z_ref.abs().sum((0, 2, 3)).max().item()
         torch.testing.assert_close(part[:, 0].sum(0), z_ref.sum((0, 2, 3)), rtol=1e-3, atol=tol)
+
+
+def test_conv_bnact_prologue_folds_residual_bn(ops):
+    """conv_bnact_fwd with res_stats: the residual is a BatchNorm's INPUT and that BN's apply is
+    folded into the staging too (a = relu(bn(y) + bn_r(y_r))) vs materialising bn_r(y_r) first."""
+    e = ops.ext()
+    torch.manual_seed(6)
+    cl = torch.channels_last
+    n, cin, cout, hw = 3, 256, 128, 13
+    y = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    yr = torch.randn_like(y)
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    r, rstats, _ = e.bn_act_fwd(yr, torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2,
+                                None, None, 0.0, 1e-5, None, False, True, None)
+    bnw, bnb = torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2
+    _, stats, _ = e.bn_act_fwd(y, bnw, bnb, None, None, 0.0, 1e-5, None, True, True, None)
+    # fp32 reference of the folded form (the materialised r is rounded to bf16 once more)
+    a_ref = torch.relu(y.float() * stats[2].view(1, -1, 1, 1) + stats[3].view(1, -1, 1, 1)
+                       + yr.float() * rstats[2].view(1, -1, 1, 1) + rstats[3].view(1, -1, 1, 1))
+    z_ref = torch.nn.functional.conv2d(a_ref, w.float())
+    cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
+    assert cfgs
+    for cfg in cfgs:
+        z, part, a, mask = e.conv_bnact_fwd(y, w, yr, stats, True, cfg, rstats)
+        torch.testing.assert_close(a.float(), a_ref, rtol=1e-2, atol=1e-2)
+        ref_bits = (a.float() > 0).permute(0, 2, 3, 1).reshape(-1, 8)
+        got = torch.stack([(mask.long() >> b) & 1 for b in range(8)], 1).bool()
+        assert torch.equal(got, ref_bits)
+        torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())
 
 
 def test_bn_finalize_part_matches_bn_act_fwd(ops):
@@ -675,7 +704,7 @@ def test_conv3x3_halo_prologues(ops, shape):
     cfgs = [c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c)]
     assert cfgs, "no 3x3 prologue config"
     for cfg in cfgs:
-        z, part, a, mask = e.conv_bnact_fwd(y, w, None, stats, False, cfg)
+        z, part, a, mask = e.conv_bnact_fwd(y, w, None, stats, False, cfg, None)
         torch.testing.assert_close(a, a_ref, rtol=0, atol=0)
         assert mask.numel() == 0
         torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 ALL_FUSIONS = frozenset({"stem_conv", "stem_stats", "split_grad", "avgpool", "igemm_conv", "conv_stats", "bn_conv",
-                         "bn_prologue", "bn_lazy_bwd", "compact_shortcut_grad"})
+                         "bn_prologue", "bn_lazy_bwd", "compact_shortcut_grad", "bn_residual_fold"})
 
 
 def _curve(disabled, steps, batches, monkeypatch):
