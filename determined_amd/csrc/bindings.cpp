@@ -81,6 +81,7 @@ extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int
                                     const float*, const float*, const float*, int, const void*, const float*,
                                     const float*, const float*, void*, uint8_t*, float*, int*, int);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
+extern "C" void damd_occupy_launch(int, double, int*, hipStream_t);
 extern "C" int damd_conv_pro_supported_w(int, int, int, int, int, int, int, int);
 extern "C" int64_t damd_conv_sk_ws_floats(int, int, int);
 extern "C" int damd_conv_sk_flag_words();
@@ -1217,6 +1218,11 @@ std::vector<at::Tensor> gelu_bwd_bias(const at::Tensor& dg, const at::Tensor& h,
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("occupy", [](int64_t nblk, double usec) {  // CU-occupancy probe on the current stream
+    static at::Tensor sink;
+    if (!sink.defined()) sink = at::empty({256}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+    damd_occupy_launch(static_cast<int>(nblk), usec, sink.data_ptr<int>(), cur_stream());
+  });
   m.def("lm_ce_fwd", &lm_ce_fwd);
   m.def("lm_ce_bwd", &lm_ce_bwd);
   m.def("bias_grad", &bias_grad);

@@ -224,7 +224,26 @@ gelu_bwd_bias_kernel(const bf16_t* __restrict__ dg, const bf16_t* __restrict__ h
 using namespace damd;
 using namespace damd::fused;
 
+// Occupancy probe: `nblk` workgroups of 256 threads that hold their CU slots for `usec`
+// microseconds (wall clock), the footprint of a collective's kernel (one workgroup per channel)
+// running next to the compute stream.  Used to measure how much the persistent conv kernels lose
+// when a side-stream kernel takes CUs (scripts/dev/interference.py); not on any training path.
+__global__ void __launch_bounds__(256) occupy_kernel(int64_t ticks, int* sink) {
+  const int64_t t0 = wall_clock64();
+  int spins = 0;
+  while (wall_clock64() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(8);
+    ++spins;
+  }
+  if (spins < 0) sink[threadIdx.x] = spins;  // keeps the loop; never taken
+}
+
 extern "C" {
+
+void damd_occupy_launch(int nblk, double usec, int* sink, hipStream_t st) {
+  // wall_clock64 runs at 100 MHz on gfx950
+  hipLaunchKernelGGL(occupy_kernel, dim3(nblk), dim3(256), 0, st, static_cast<int64_t>(usec * 100.0), sink);
+}
 
 void damd_lm_ce_fwd_launch(const void* logits, const int64_t* labels, int64_t rows, int T, int V, int Vp,
                            int64_t ignore_index, float* row_loss, float* lse, hipStream_t st) {
