@@ -28,6 +28,8 @@
 // K = 64 layers (one k-step per tile) still overlap their loads with the previous tile's MFMAs
 // and stores.
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace damd {
@@ -1630,6 +1632,17 @@ int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, 
   return 1;
 }
 
+// DAMD_CONV_OVERSUB=k: k x the resident grid for the (non-stream-K) persistent configs, so blocks
+// displaced by a concurrent kernel (a collective on another stream) leave work the others pick up
+int conv_oversub() {
+  static const int k = [] {
+    const char* e = getenv("DAMD_CONV_OVERSUB");
+    const int v = e != nullptr ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  return k;
+}
+
 // groups (pixel-tile strides) for a config; also the leading dim of the stats partials
 int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
   const Cfg c = kCfgs[cfg];
@@ -1637,7 +1650,7 @@ int damd_conv_groups(int64_t M, int K, int W, int cfg, int groups_override) {
   const int ctiles = K / c.bco;
   if (c.sk) return 256 * blocks_per_cu(c, W) / ctiles;  // the resident grid; plans may leave blocks idle
   int64_t groups = groups_override > 0 ? groups_override
-                                       : (256LL * blocks_per_cu(c, W) + ctiles - 1) / ctiles;
+                                       : (256LL * blocks_per_cu(c, W) + ctiles - 1) / ctiles * conv_oversub();
   if (groups > ptiles) groups = ptiles;
   if (groups < 1) groups = 1;
   return static_cast<int>(groups);
