@@ -25,6 +25,10 @@ MI355X design points:
   all-reduce of S bytes moves 2*(7/8)*S per rank over point-to-point links; 16 MiB keeps
   each collective bandwidth-bound (>> its ~20-40 us launch/latency floor) while leaving
   enough buckets (ResNet-50 bf16: 51 MB of grads -> 4-5 collectives) to overlap backward.
+* The LAST bucket (the earliest layers' gradients, ready only when the backward ends) is capped
+  at ``last_bucket_mb`` (2 MiB) too: its all-reduce cannot overlap anything, so it should be
+  small -- a 16 MiB tail bucket holding layer3/layer2 weights of ResNet-50 would wait for the
+  stem's gradient and then run fully exposed.
 * Averaging uses ``ReduceOp.AVG`` on RCCL (no separate divide kernel); gloo (CPU tests)
   falls back to SUM + in-place divide.
 """
@@ -83,6 +87,7 @@ class DistributedDataParallel(nn.Module):
         process_group: Optional[dist.ProcessGroup] = None,
         bucket_cap_mb: float = 16.0,
         first_bucket_mb: float = 2.0,
+        last_bucket_mb: float = 2.0,
         broadcast_buffers: bool = False,
         average: bool = True,
         reorder_after_first_step: bool = True,
@@ -93,6 +98,7 @@ class DistributedDataParallel(nn.Module):
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.bucket_cap = int(bucket_cap_mb * MiB)
         self.first_bucket_cap = int(first_bucket_mb * MiB)
+        self.last_bucket_cap = int(min(last_bucket_mb, bucket_cap_mb) * MiB)
         self.broadcast_buffers = broadcast_buffers
         self.average = average
         self._reorder = reorder_after_first_step
@@ -146,12 +152,26 @@ class DistributedDataParallel(nn.Module):
                 cur, cur_bytes = [], 0
                 cap = self.bucket_cap
 
+        # the tail (last-ready gradients) forms its own small bucket: peel it off the end first
+        order = list(order)
+        tail: List[nn.Parameter] = []
+        tail_bytes = 0
+        while order and self.last_bucket_cap > 0:
+            p = order[-1]
+            nbytes = p.numel() * p.element_size()
+            if tail and (p.dtype != tail[0].dtype or p.device != tail[0].device
+                         or tail_bytes + nbytes > self.last_bucket_cap):
+                break
+            tail.insert(0, order.pop())
+            tail_bytes += nbytes
         for p in order:
             nbytes = p.numel() * p.element_size()
             if cur and (p.dtype != cur[0].dtype or p.device != cur[0].device or cur_bytes + nbytes > cap):
                 flush()
             cur.append(p)
             cur_bytes += nbytes
+        flush()
+        cur, cur_bytes = tail, tail_bytes
         flush()
         for b in self._buckets:
             for p, v in zip(b.params, b.views):

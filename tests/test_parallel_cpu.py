@@ -120,3 +120,27 @@ def test_ddp_no_sync_before_first_step_keeps_bucket_order_clean():
     ref(x).square().sum().backward()
     for a, b in zip(g, [p.grad for p in model.parameters()]):
         torch.testing.assert_close(a, b)
+
+
+def test_ddp_tail_bucket_is_small():
+    """The last-ready gradients (the first layers) form their own bucket of at most
+    ``last_bucket_mb``: its all-reduce is the one that cannot overlap the backward."""
+    from determined_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(512, 512), torch.nn.Linear(512, 512), torch.nn.Linear(512, 512),
+                            torch.nn.Linear(512, 8))
+    mib = 1 << 20
+    ddp = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_mb=0.01, last_bucket_mb=1.2)
+    sizes = [b.numel * 4 for b in ddp._buckets]
+    assert sizes[-1] <= 1.2 * mib and sizes[0] <= 0.02 * mib + 16 * 1024, sizes
+    # the tail holds the first layer's parameters (ready last in the backward)
+    assert ddp._buckets[-1].params[-1] is m[0].weight or ddp._buckets[-1].params[0] is m[0].bias
+    x = torch.randn(4, 512)
+    m2 = torch.nn.Sequential(*[torch.nn.Linear(l.in_features, l.out_features) for l in m])
+    m2.load_state_dict(m.state_dict())
+    ddp(x).square().sum().backward()
+    ddp.finish()
+    m2(x).square().sum().backward()
+    for p, q in zip(m.parameters(), m2.parameters()):
+        torch.testing.assert_close(p.grad, q.grad)
