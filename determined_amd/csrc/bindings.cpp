@@ -466,6 +466,27 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, dres};
 }
 
+// BN backward (no ReLU, no residual) without its apply pass: reduce + finalize of dz over x ->
+// (coef [3, C] with dx = A*dz + B*x + Cc, dgamma, dbeta); the apply runs in the consumer's operand
+// staging (conv_fwd_pro2, ops/conv.py _LazyBNGrad).
+std::vector<at::Tensor> bn_bwd_coef(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& stats,
+                                    const at::Tensor& weight) {
+  check_bn_tensor(dz, x, "dz");
+  const int64_t C = bn_channels(x);
+  const int64_t M = x.numel() / C;
+  auto fopts = x.options().dtype(at::kFloat);
+  const int nb = damd_bn_num_blocks(M, static_cast<int>(C));
+  auto part = at::empty({nb, 2, C}, fopts);
+  auto coef = at::empty({3, C}, fopts);
+  auto dgamma = at::empty({C}, weight.options());
+  auto dbeta = at::empty({C}, weight.options());
+  damd_bn_bwd_launch(dz.data_ptr(), x.data_ptr(), nullptr, M, static_cast<int>(C), stats[0].data_ptr<float>(),
+                     stats[1].data_ptr<float>(), stats[2].data_ptr<float>(), stats[3].data_ptr<float>(),
+                     part.data_ptr<float>(), coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(), nullptr,
+                     nullptr, 0, dtype_code(x), dtype_code(weight), cur_stream(), nullptr, nullptr);
+  return {coef, dgamma, dbeta};
+}
+
 // BN backward finalize only: (coef [3, C] = A, B, Cc with dx = A*dz + B*x + Cc, dgamma, dbeta)
 std::vector<at::Tensor> bn_bwd_finalize_part(const at::Tensor& x, const at::Tensor& stats, const at::Tensor& weight,
                                              const at::Tensor& part) {
@@ -967,6 +988,37 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
   return {dz, part};
 }
 
+// Stride-1 1x1 input gradient whose operand is a deferred BN backward: dX = conv1x1(dy, wt) with
+// dy = coef[0] * dz + coef[1] * y + coef[2] formed in the operand staging (PRO 2) and returned
+// materialised for the weight gradient: (dX, dy).  No epilogue.
+std::vector<at::Tensor> conv_fwd_pro2(const at::Tensor& dz, const at::Tensor& wt, const at::Tensor& y,
+                                      const at::Tensor& coef, int64_t cfg) {
+  TORCH_CHECK(wt.dim() == 4 && wt.size(2) == 1 && wt.size(3) == 1 && conv_supported(dz, wt, cfg, 1, 0),
+              "conv_fwd_pro2: unsupported input / weight / config");
+  const int64_t N = dz.size(0), C = dz.size(1), H = dz.size(2), W = dz.size(3), K = wt.size(0);
+  TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(W),
+                                        static_cast<int>(cfg)), "conv_fwd_pro2: config has no prologue variant");
+  TORCH_CHECK(y.sizes() == dz.sizes() && y.strides() == dz.strides() && y.scalar_type() == at::kBFloat16,
+              "conv_fwd_pro2: y must match dz");
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.dim() == 2 && coef.size(0) == 3 && coef.size(1) == C &&
+              coef.is_contiguous(), "conv_fwd_pro2: coef must be float32 [3, C]");
+  const int64_t M = N * H * W;
+  TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_fwd_pro2: tensor too large");
+  auto wl = wt.contiguous(at::MemoryFormat::ChannelsLast);
+  auto out = at::empty({N, K, H, W}, dz.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto dyo = at::empty_like(dz);
+  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
+  const SkWorkspace sk = sk_workspace(dz, K, W, cfg);
+  const int rc = damd_conv_fwd_launch(dz.data_ptr(), wl.data_ptr(), out.data_ptr(), nullptr, static_cast<int>(N),
+                                      static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(K),
+                                      1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 0, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, nullptr, 2, y.data_ptr(), coef[0].data_ptr<float>(),
+                                      coef[2].data_ptr<float>(), coef[1].data_ptr<float>(), dyo.data_ptr(), nullptr,
+                                      sk.wsp, sk.flags, 0);
+  TORCH_CHECK(rc == 0, "conv_fwd_pro2: launch rejected");
+  return {out, dyo};
+}
+
 // dW of the convolution y = conv(x, w) (stride, pad) from dY, in w's dtype, as a channels-last
 // [K, C, R, S] tensor (physically [K][R][S][C]).
 bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t K, int64_t cfg) {
@@ -1237,6 +1289,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_from_part", &bn_bwd_from_part);
   m.def("bn_finalize_part", &bn_finalize_part);
   m.def("bn_bwd_finalize_part", &bn_bwd_finalize_part);
+  m.def("bn_bwd_coef", &bn_bwd_coef);
+  m.def("conv_fwd_pro2", &conv_fwd_pro2);
   m.def("bn_bwd_apply_coef", &bn_bwd_apply_coef);
   m.def("bn_apply", &bn_apply);
   m.def("bn_pool_fwd", &bn_pool_fwd);

@@ -839,6 +839,10 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
+  if (dx == nullptr) {  // coefficients only: the apply pass is deferred to the consumer (bn_bwd_coef)
+    DAMD_CHECK_LAUNCH();
+    return;
+  }
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));

@@ -40,7 +40,7 @@ def _downsample(ds: nn.Module, x: torch.Tensor, lazy_bn: bool = False):
             and not ds[1]._forward_pre_hooks):
         y, part = conv_bn_input(ds[0], x)
         if lazy_bn and part is not None and not ds[1].act and ds[1].kernel_path(y):
-            return LazyBNResidual(y, part, ds[1])
+            return LazyBNResidual(y, part, ds[1], ds[0])
         return ds[1](y, stats_part=part)
     return ds(x)
 

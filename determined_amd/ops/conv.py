@@ -340,11 +340,30 @@ class _IGemmConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dpart=None):
+        from determined_amd import ops
+
         x, weight = ctx.saved_tensors
         stride, pad, compact = ctx.geo
-        dy = dy.contiguous(memory_format=torch.channels_last)
+        parked = _LazyBNGrad.take(dy)  # a folded shortcut BN's deferred backward apply (LazyBNResidual)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        if parked is not None:
+            e = ops.ext()
+            wt = _flip_weight(weight)
+            cfgs = ([c for c in range(e.conv_num_cfgs())
+                     if e.conv_pro_supported(parked.dz, wt, c) and _allowed("dgrad_pro2", c)]
+                    if weight.shape[2] == 1 and weight.shape[3] == 1 and pad == 0 and ctx.needs_input_grad[0] else [])
+            if cfgs:  # dX with dy = A*dz + B*y + Cc formed in the operand staging; dy returned for dW
+                cands = {c: (lambda c=c: e.conv_fwd_pro2(parked.dz, wt, parked.y, parked.coef, c)) for c in cfgs}
+                key = ("dgrad_pro2", tuple(parked.dz.shape), tuple(weight.shape))
+                dxo, dy = cands[_pick(key, cands, default=cfgs[-1])]()
+                if compact:
+                    dx = _StridedGrad.park(x, dxo)
+                else:  # stride 1: dxo is dX; stride 2 (pad 0): dX is dxo at the even pixels
+                    dx = dxo if stride == 1 else _StridedGrad.materialise(dxo, x.shape)
+            else:
+                dy = parked.materialise()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if ctx.needs_input_grad[0] and dx is None:
             if compact:  # dX on the output grid: the stride-1 1x1 input gradient of dY
                 xc = torch.empty((x.shape[0], x.shape[1]) + tuple(dy.shape[2:]), device=x.device, dtype=x.dtype,
                                  memory_format=torch.channels_last)  # shape only (MIOpen candidate)
@@ -449,8 +468,16 @@ class LazyBNResidual:
     folds into that staging (a = relu(bn(x) + y * r_scale + r_shift); conv_igemm.hip ProArgs
     ``rscale``) and ``r`` is never written; any other consumer calls :meth:`materialise`."""
 
-    def __init__(self, y: torch.Tensor, part: Optional[torch.Tensor], bn: nn.Module):
-        self.y, self.part, self.bn = y, part, bn
+    def __init__(self, y: torch.Tensor, part: Optional[torch.Tensor], bn: nn.Module, conv: Optional[nn.Module] = None):
+        self.y, self.part, self.bn, self.conv = y, part, bn, conv
+
+    def defer_bwd(self) -> bool:
+        """Whether this BN's backward apply can move into the producing conv's input gradient:
+        ``y`` came out of a 1x1 :class:`_IGemmConvFn` node (its only consumer is the fold)."""
+        from determined_amd import ops
+
+        return (self.conv is not None and self.conv.kernel_size == (1, 1) and self.conv.padding == (0, 0)
+                and isinstance(self.y.grad_fn, _IGemmConvFn._backward_cls) and ops.fusion_enabled("bn_lazy_bwd"))
 
     def materialise(self) -> torch.Tensor:
         return self.bn(self.y, stats_part=self.part)
@@ -478,8 +505,9 @@ class _BNActConvFn(torch.autograd.Function):
 
         e = ops.ext()
         rstats = None
+        ctx.res_defer = False
         if res_w is not None:  # residual = bn_r(residual) folded into the prologue (LazyBNResidual)
-            r_rm, r_rv, r_mom, r_eps, r_part = res_args
+            r_rm, r_rv, r_mom, r_eps, r_part, ctx.res_defer = res_args
             rstats = e.bn_finalize_part(r_part, residual.numel() // residual.shape[1], res_w, res_b, r_rm, r_rv,
                                         float(r_mom), float(r_eps))
         if pro:  # 1x1 conv applies the BN(+residual)+ReLU while staging its input (conv_igemm.hip PRO)
@@ -603,7 +631,11 @@ class _BNActConvFn(torch.autograd.Function):
         dg_r = db_r = None
         if rstats is not None and dres is not None:  # backward of the folded residual BN (no ReLU)
             dres = dres.contiguous(memory_format=cl)
-            dres, dg_r, db_r, _ = e.bn_act_bwd(dres, res_in, None, rstats, res_w, False, False, None, None)
+            if ctx.res_defer:  # its apply pass moves into the shortcut conv's input gradient (PRO 2)
+                coef, dg_r, db_r = e.bn_bwd_coef(dres, res_in, rstats, res_w)
+                dres = _LazyBNGrad.park(dres, res_in, coef)
+            else:
+                dres, dg_r, db_r, _ = e.bn_act_bwd(dres, res_in, None, rstats, res_w, False, False, None, None)
         return (dy, dg, db, None, None, dres if has_res else None, None, None, None, dw, None, None, None, None, None,
                 dg_r, db_r, None)
 
@@ -668,7 +700,7 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                 r_rm, r_rv, r_mom = lres.bn.train_step_args()
                 return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, rt, momentum, bn.eps, stats_part, w, st,
                                           pad, cfg, True, lazy, lres.bn.weight, lres.bn.bias,
-                                          (r_rm, r_rv, r_mom, lres.bn.eps, lres.part))
+                                          (r_rm, r_rv, r_mom, lres.bn.eps, lres.part, lres.defer_bwd()))
             return _BNActConvFn.apply(y, bn.weight, bn.bias, rm, rv, residual, momentum, bn.eps, stats_part, w, st,
                                       pad, cfg, True, lazy)
         key = ("fwd", tuple(y.shape), tuple(w.shape), st, pad)

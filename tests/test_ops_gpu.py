@@ -641,6 +641,34 @@ def test_conv_bnact_prologue_folds_residual_bn(ops):
         torch.testing.assert_close(z.float(), z_ref, rtol=2e-2, atol=2e-2 * z_ref.abs().max().item())
 
 
+def test_bn_bwd_coef_and_conv_fwd_pro2_match_unfused(ops):
+    """Deferred backward of a BN without ReLU (the downsample BN): bn_bwd_coef (reduce + finalize
+    only) + conv_fwd_pro2 (1x1 input gradient forming dy = A*dz + B*y + Cc in its staging) vs
+    bn_act_bwd's dx followed by the plain input-gradient conv."""
+    e = ops.ext()
+    torch.manual_seed(8)
+    cl = torch.channels_last
+    n, k, c, hw = 3, 256, 128, 11
+    y = torch.randn(n, k, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    dz = torch.randn_like(y)
+    bw = (torch.rand(k, device="cuda") + 0.5)
+    _, stats, _ = e.bn_act_fwd(y, bw, torch.randn(k, device="cuda") * 0.2, None, None, 0.0, 1e-5, None, False, True,
+                               None)
+    dy_ref, dg_ref, db_ref, _ = e.bn_act_bwd(dz, y, None, stats, bw, False, False, None, None)
+    coef, dg, db = e.bn_bwd_coef(dz, y, stats, bw)
+    torch.testing.assert_close(dg, dg_ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, db_ref, rtol=1e-4, atol=1e-3)
+    w = (torch.randn(k, c, 1, 1, device="cuda") / k ** 0.5).to(torch.bfloat16)
+    wt = w.transpose(0, 1).contiguous(memory_format=cl)
+    dx_ref = torch.nn.grad.conv2d_input((n, c, hw, hw), w.float(), dy_ref.float())
+    cfgs = [q for q in range(e.conv_num_cfgs()) if e.conv_pro_supported(dz, wt, q)]
+    assert cfgs
+    for cfg in cfgs:
+        dx, dy = e.conv_fwd_pro2(dz, wt, y, coef, cfg)
+        torch.testing.assert_close(dy.float(), dy_ref.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(dx.float(), dx_ref, rtol=2e-2, atol=2e-2 * dx_ref.abs().max().item())
+
+
 def test_bn_finalize_part_matches_bn_act_fwd(ops):
     e = ops.ext()
     torch.manual_seed(1)
