@@ -224,7 +224,17 @@ def _flip_weight(w: torch.Tensor) -> torch.Tensor:
     (one copy kernel instead of a flip kernel + a copy per backward)."""
     if w.shape[2] == 1 and w.shape[3] == 1:
         return w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
+    k, c, r, s = w.shape
+    if w.is_contiguous(memory_format=torch.channels_last):  # one gather: [K][RS][C] -> [C][RS reversed][K]
+        rev = _REV_TAPS.get((r * s, w.device))
+        if rev is None:
+            rev = _REV_TAPS[(r * s, w.device)] = torch.arange(r * s - 1, -1, -1, device=w.device)
+        out = torch.index_select(w.permute(0, 2, 3, 1).reshape(k, r * s, c).permute(2, 1, 0), 1, rev)
+        return out.view(c, r, s, k).permute(0, 3, 1, 2)
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+_REV_TAPS: Dict[tuple, torch.Tensor] = {}
 
 
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
@@ -669,10 +679,9 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                     and 2 * pad == w.shape[2] - 1
                     and (residual is None or w.shape[2] == 1) else [])  # 3x3 prologue: no residual
         if pro_cfgs and w.shape[2] != 1:
-            dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
-            dummy[2].fill_(1.0)
-
-            def t_fused() -> float:
+            def t_fused() -> float:  # (only runs when the choice is not cached yet)
+                dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
+                dummy[2].fill_(1.0)
                 return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, None, dummy, False, c, None)) for c in pro_cfgs)
 
             def t_plain() -> float:

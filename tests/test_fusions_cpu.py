@@ -156,3 +156,15 @@ def test_conv_tune_db_roundtrip(tmp_path, monkeypatch):
     # a shipped choice is used only if it is one of the candidates of this build
     monkeypatch.setattr(conv, "_DB_LOADED", True)
     assert conv._pick(("fwd", (512, 64, 56, 56), (64, 64, 3, 3), 1, 1), {3: None, 7: None}, 3) == 7
+
+
+def test_flip_weight_matches_flip_transpose():
+    """The dgrad weights (flipped taps, transposed channels, channels-last) from the single gather
+    equal flip(2, 3).transpose(0, 1)."""
+    from determined_amd.ops.conv import _flip_weight
+
+    for shp in [(64, 32, 3, 3), (128, 64, 1, 1), (8, 16, 7, 7)]:
+        w = torch.randn(*shp).contiguous(memory_format=torch.channels_last)
+        ref = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        out = _flip_weight(w)
+        assert torch.equal(out, ref) and out.is_contiguous(memory_format=torch.channels_last)
