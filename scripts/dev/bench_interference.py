@@ -47,4 +47,9 @@ if spec:
     D.DistributedDataParallel._complete = _complete
     D.DistributedDataParallel.finish = finish
 
+if os.environ.get("DAMD_SIM_HIPRIO"):  # compute on a high-priority stream (collectives keep normal priority)
+    hi = torch.cuda.Stream(device=int(os.environ.get("LOCAL_RANK", "0")), priority=-1)
+    with torch.cuda.stream(hi):
+        rc = bench.main()
+    sys.exit(rc)
 sys.exit(bench.main())
