@@ -24,7 +24,16 @@ sys.path.insert(0, ROOT)
 # MIOpen find-db of the ResNet-50 convolutions measured on MI355X (written by MIOpen itself when
 # torch.backends.cudnn.benchmark searches): a fresh box reuses it instead of re-searching every
 # conv solver on every rank during warm-up.
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(ROOT, "determined_amd", "benchmarks", "miopen_db"))
+_MIOPEN_DB = os.path.join(ROOT, "determined_amd", "benchmarks", "miopen_db")
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "MIOPEN_USER_DB_PATH" not in os.environ:
+    # one private copy per rank: N processes never write the same find-db files concurrently
+    import shutil
+    import tempfile
+
+    _priv = os.path.join(tempfile.gettempdir(), f"damd_miopen_db_rank{os.environ.get('LOCAL_RANK', '0')}_{os.getpid()}")
+    shutil.copytree(_MIOPEN_DB, _priv, dirs_exist_ok=True)
+    _MIOPEN_DB = _priv
+os.environ.setdefault("MIOPEN_USER_DB_PATH", _MIOPEN_DB)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
