@@ -62,14 +62,27 @@ def parse() -> argparse.Namespace:
 
 def main() -> int:
     a = parse()
+    # stdout carries exactly one line (rank 0's JSON): everything else written to fd 1 during the
+    # run -- e.g. gloo's "[Gloo] Rank i is connected to ..." lines, printed by every rank when the
+    # harness builds its gloo side groups -- goes to stderr
+    sys.stdout.flush()
+    stdout_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    torch.cuda.set_device(local)
+    # one rank per GPU; the modulo and DAMD_BENCH_BACKEND=gloo only matter for rehearsing the
+    # multi-rank path with several ranks on one GPU (RCCL refuses two ranks on one device)
+    dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     torch.backends.cudnn.benchmark = bool(a.conv_benchmark)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("DAMD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     from determined_amd.benchmarks.resnet50 import build_step
 
@@ -155,7 +168,10 @@ def main() -> int:
                 "final_loss": round(loss, 4),
             },
         }
+        sys.stdout.flush()
+        os.dup2(stdout_fd, 1)
         print(json.dumps(out), flush=True)
+        os.dup2(2, 1)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
