@@ -168,3 +168,23 @@ def test_flip_weight_matches_flip_transpose():
         ref = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
         out = _flip_weight(w)
         assert torch.equal(out, ref) and out.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_lazy_bn_residual_and_strided_grad_fallbacks_on_cpu():
+    """Off the GPU kernels a LazyBNResidual is materialised (bn(y)) before the plain composition,
+    and a compact stride-2 gradient expands to the full grid with zeros at the odd pixels."""
+    from determined_amd.ops.bn import BatchNormAct2d
+    from determined_amd.ops.conv import LazyBNResidual, _StridedGrad, bn_act_conv
+
+    torch.manual_seed(0)
+    bn, bnr = BatchNormAct2d(8), BatchNormAct2d(8, act=False)
+    conv = torch.nn.Conv2d(8, 4, 1, bias=False)
+    y, yr = torch.randn(2, 8, 5, 5), torch.randn(2, 8, 5, 5)
+    a, z, part = bn_act_conv(bn, y, None, LazyBNResidual(yr, None, bnr), conv)
+    bn2, bnr2 = BatchNormAct2d(8), BatchNormAct2d(8, act=False)
+    a_ref = bn2(y, bnr2(yr))
+    torch.testing.assert_close(a, a_ref)
+    torch.testing.assert_close(z, conv(a_ref))
+    c = torch.randn(2, 3, 3, 3)
+    full = _StridedGrad.materialise(c, (2, 3, 5, 5))
+    assert torch.equal(full[:, :, ::2, ::2], c) and full[:, :, 1::2].abs().sum() == 0 and full[:, :, :, 1::2].abs().sum() == 0
