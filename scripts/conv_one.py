@@ -16,6 +16,7 @@ for n in ("cin", "cout", "k", "stride", "hw", "cfg"):
     ap.add_argument(n, type=int)
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--mode", default="fwd", choices=["fwd", "dgrad_bn_pro"])
 a = ap.parse_args()
 from determined_amd import ops  # noqa: E402
 
@@ -25,7 +26,21 @@ x = torch.randn(a.batch, a.cin, a.hw, a.hw, device="cuda").to(torch.bfloat16).co
 w = torch.randn(a.cout, a.cin, a.k, a.k, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
 pad = a.k // 2
 assert e.conv_supported(x, w, a.cfg, a.stride, pad)
-for _ in range(a.iters):
-    e.conv_fwd(x, w, a.stride, pad, True, a.cfg, 0)
+if a.mode == "dgrad_bn_pro":
+    # 1x1 input gradient of a chained ResNet block: operand dy = A*dz + B*y + Cc formed in the
+    # staging (x = dz, yn = y), BN-backward epilogue with the ReLU bit mask and the shortcut gradient
+    assert a.k == 1 and a.stride == 1 and e.conv_pro_supported(x, w, a.cfg)
+    yn = torch.randn_like(x)
+    coef = torch.randn(3, a.cin, device="cuda").contiguous()
+    yb = torch.randn(a.batch, a.cout, a.hw, a.hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    res = torch.randn_like(yb)
+    _, stats, mask = e.bn_act_fwd(yb, torch.rand(a.cout, device="cuda") + 0.5, torch.randn(a.cout, device="cuda"),
+                                  None, None, 0.0, 1e-5, res, True, True, None)
+    d2 = torch.randn_like(yb)
+    for _ in range(a.iters):
+        e.conv_dgrad_bn(x, w, 0, a.cfg, d2, yb, mask, stats, yn, coef)
+else:
+    for _ in range(a.iters):
+        e.conv_fwd(x, w, a.stride, pad, True, a.cfg, 0)
 torch.cuda.synchronize()
 print("ok")
