@@ -46,8 +46,10 @@ def parse() -> argparse.Namespace:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
-    # 512 images per GPU: +7% samples/s over 256 on MI355X (measured), ~60 GB of the 288 GB HBM
-    p.add_argument("--batch", type=int, default=512, help="per-GPU batch size")
+    # 1024 images per GPU (~120 GB of the 288 GB HBM3E): same box, current kernels, 20 steps:
+    # 256 -> 12,526, 512 -> 14,050, 1024 -> 15,180 samples/s (profiles/resnet50_batch_sweep_1gpu.jsonl);
+    # the larger pixel count fills the 14x14 / 7x7 layers' tiles across the 256 CUs
+    p.add_argument("--batch", type=int, default=1024, help="per-GPU batch size")
     p.add_argument("--variant", default="bf16_master", choices=["bf16_master", "amp", "bf16_fp32bn"])
     p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
     p.add_argument("--bucket-mb", type=float, default=16.0)
