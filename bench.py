@@ -115,6 +115,9 @@ def main() -> int:
             print(f"[bench] warmup {i + 1}/{a.warmup} {time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
     warm_done.set()
     torch.cuda.synchronize()
+    import determined_amd.ops as damd_ops
+
+    damd_ops.conv_health_check()  # a stream-K hand-off time-out fails the run loudly
     if a.save_tune_db and rank == 0:
         from determined_amd.ops.conv import save_tune_db
 
@@ -135,6 +138,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    damd_ops.conv_health_check()
     loss = float(state["last_loss"]()) if "last_loss" in state else float("nan")
     if rank == 0 and os.environ.get("DAMD_TUNE_DUMP"):  # per-layer kernel choices (A/B analysis)
         from determined_amd.ops.conv import tuned_choices

@@ -262,7 +262,11 @@ class SlurmBackend(_BatchBackend):
         return _run(["sbatch", "--parsable", str(script)]).strip().split(";")[0]
 
     def exit_code(self, job_id: str, workdir: pathlib.Path) -> Optional[int]:
-        state = _run(["squeue", "-h", "-j", job_id, "-o", "%T"]).strip()
+        purged = False
+        try:
+            state = _run(["squeue", "-h", "-j", job_id, "-o", "%T"]).strip()
+        except RuntimeError as e:  # purged after MinJobAge ("Invalid job id specified"): no longer queued
+            state, purged = "", "invalid job id" in str(e).lower()
         if state and state.split()[0] not in ("COMPLETED", "FAILED", "CANCELLED", "TIMEOUT", "NODE_FAIL",
                                               "OUT_OF_MEMORY", "PREEMPTED", "BOOT_FAIL", "DEADLINE"):
             return None
@@ -274,7 +278,7 @@ class SlurmBackend(_BatchBackend):
         except Exception:
             acct = []
         if not acct:
-            return None if not state else 1
+            return None if not (state or purged) else 1
         st, _, ec = acct[0].partition("|")
         rc = int(ec.split(":")[0] or 0) if ec else 0
         if st.startswith("CANCELLED"):

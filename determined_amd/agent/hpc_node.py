@@ -76,8 +76,12 @@ def kubernetes_layout(env: Dict[str, str]) -> Tuple[int, List[str]]:
     from determined_amd.common.api import Session
 
     sess = Session(env["DET_MASTER"], token=env.get("DET_SESSION_TOKEN") or None)
+    # one uuid per call: Session's retries re-send the same body, so a post whose response was lost
+    # re-fetches the finished round; a restarted pod (new address) joins a new round
+    import uuid
+
     got = sess.post(f"/api/v1/allocations/{env['DET_ALLOCATION_ID']}/all_gather",
-                    {"request_uuid": f"rank-{rank}", "num_peers": npods, "rank": rank, "data": me,
+                    {"request_uuid": f"rank-{rank}-{uuid.uuid4().hex}", "num_peers": npods, "rank": rank, "data": me,
                      "timeout_seconds": 1800}, timeout=1900)
     return rank, list(got["data"])
 

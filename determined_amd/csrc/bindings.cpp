@@ -766,20 +766,29 @@ at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::
 
 // ---------------------------------------------------------------- implicit-GEMM convolution
 // Stream-K configs (conv_igemm.hip make_plan) hand partial tiles between blocks: a per-call fp32
-// slab workspace from the caching allocator (stream-ordered reuse) and a per-device buffer of flag
-// words that the kernels leave zeroed (+ a poll time-out counter at its end).  The convolutions
-// of one device run on one stream at a time, so the flag buffer is not shared between live launches.
+// slab workspace from the caching allocator (stream-ordered reuse) and a buffer of flag words per
+// (device, stream) that the kernels leave zeroed (+ a poll time-out counter at its end).  Launches
+// on one stream are ordered, so one buffer per stream is never shared between live launches;
+// stream-K convs issued from two streams at once get separate buffers.
 struct SkWorkspace {
   at::Tensor ws;
   float* wsp = nullptr;
   int* flags = nullptr;
 };
 
-at::Tensor& sk_flag_buffer(const at::Device& dev) {
+std::mutex& sk_mutex() {
   static std::mutex mu;
-  static std::map<int, at::Tensor> bufs;
-  std::lock_guard<std::mutex> lk(mu);
-  at::Tensor& t = bufs[dev.index()];
+  return mu;
+}
+
+std::map<std::pair<int, hipStream_t>, at::Tensor>& sk_flag_buffers() {
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> bufs;
+  return bufs;
+}
+
+at::Tensor sk_flag_buffer(const at::Device& dev, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(sk_mutex());
+  at::Tensor& t = sk_flag_buffers()[{static_cast<int>(dev.index()), stream}];
   if (!t.defined()) t = at::zeros({damd_conv_sk_flag_words()}, at::TensorOptions().device(dev).dtype(at::kInt));
   return t;
 }
@@ -790,14 +799,30 @@ SkWorkspace sk_workspace(const at::Tensor& like, int64_t K, int64_t W, int64_t c
   if (n == 0) return s;
   s.ws = at::empty({n}, like.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
   s.wsp = s.ws.data_ptr<float>();
-  s.flags = sk_flag_buffer(like.device()).data_ptr<int>();
+  s.flags = sk_flag_buffer(like.device(), cur_stream()).data_ptr<int>();
   return s;
 }
 
-// poll time-outs recorded by stream-K launches on this device (0 unless a hand-off never arrived)
-int64_t conv_sk_timeouts(const at::Tensor& like) {
-  at::Tensor& t = sk_flag_buffer(like.device());
-  return t.narrow(0, damd_conv_sk_flag_words() - 16, 1).item<int>();
+// Poll time-outs recorded by stream-K launches on this device, over every stream (0 unless a
+// hand-off never arrived; such a tile was written as NaN).  Synchronises the device.  With
+// reset=true the flag words and counters are zeroed afterwards (a timed-out consumer leaves its
+// producer's flag set), so the buffers are clean for later launches.
+int64_t conv_sk_timeouts(const at::Tensor& like, bool reset) {
+  std::vector<at::Tensor> bufs;
+  {
+    std::lock_guard<std::mutex> lk(sk_mutex());
+    for (auto& kv : sk_flag_buffers())
+      if (kv.first.first == like.device().index()) bufs.push_back(kv.second);
+  }
+  if (bufs.empty()) return 0;
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "conv_sk_timeouts: device synchronize failed");
+  int64_t n = 0;
+  for (auto& t : bufs) n += t.narrow(0, damd_conv_sk_flag_words() - 16, 1).item<int>();
+  if (reset && n > 0) {
+    for (auto& t : bufs) t.zero_();
+    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "conv_sk_timeouts: device synchronize failed");
+  }
+  return n;
 }
 
 // x: [N, C, H, W] bf16 channels-last; w: [K, C, R, S] bf16 (made channels-last = [K][R][S][C]);
@@ -1309,7 +1334,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported);
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
-  m.def("conv_sk_timeouts", &conv_sk_timeouts);
+  m.def("conv_sk_timeouts", &conv_sk_timeouts, py::arg("like"), py::arg("reset") = false);
   m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
   m.def("wgrad_supported", &wgrad_supported);

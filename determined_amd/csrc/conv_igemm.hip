@@ -292,7 +292,9 @@ __device__ __forceinline__ void epi_flush_sums(float (&st_s)[FI / 2][8], float (
 // a relaxed agent-scope atomic store; the consumer's lane 0 polls relaxed, takes ONE agent acquire,
 // resets the flag for the next launch, and after a barrier every wave reads the slabs with plain
 // loads.  Every block publishes before it waits, and only waits on earlier blocks of its own XCD
-// slice (dispatched before it), so the chain always drains; the poll is bounded anyway (sk.err).
+// slice (dispatched before it), so the chain always drains; the poll is bounded anyway: a time-out
+// counts in sk.err and fills the tile with NaN (never a silently wrong output); the host checks
+// the counter (ops.conv_health_check) after tuning and at reporting boundaries, and raises.
 struct SkArgs {
   float* ws;   // [nblk][BCO * BP] fp32 slabs, slot = the block's remapped id
   int* flags;  // [nblk] 0 / 1, zero between launches (the consumer resets them)
@@ -388,23 +390,40 @@ template <int FI, int FJ, int NT>
 __device__ __forceinline__ void sk_gather(f4 (&acc)[FI][FJ], const SkArgs& sk, const Plan& p, int pt, int units,
                                           int ctiles, int ct) {
   const int64_t t0u = static_cast<int64_t>(pt - p.p0) * units;  // the tile's first unit in the slice
+  __shared__ int sk_bad;  // a hand-off that never arrived: the tile's output is poisoned (NaN)
   if (threadIdx.x == 0) {
+    int bad = 0;
     for (int jj = p.j - 1; jj >= 0; --jj) {
       const int64_t r0 = jj * p.U / p.gpx, r1 = (jj + 1) * p.U / p.gpx;
       if (r1 <= t0u) break;
       if (r0 >= r1) continue;
       int* f = sk.flags + (p.xs * p.gpx + jj) * ctiles + ct;
       unsigned spins = 0;
+      bool arrived = true;
       while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 20)) { atomicAdd(sk.err, 1); break; }
+        if (++spins > (1u << 20)) { arrived = false; break; }
       }
-      __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      if (arrived) {
+        __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      } else {  // the flag is left as is: the host sees sk.err, resets the flags and raises
+        __hip_atomic_fetch_add(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bad = 1;
+      }
     }
+    sk_bad = bad;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  if (sk_bad) {  // never a silently wrong tile: NaN propagates into the loss
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) acc[i][j] = f4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                                                  __builtin_nanf("")};
+    return;
+  }
   for (int jj = p.j - 1; jj >= 0; --jj) {
     const int64_t r0 = jj * p.U / p.gpx, r1 = (jj + 1) * p.U / p.gpx;
     if (r1 <= t0u) break;

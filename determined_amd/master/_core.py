@@ -42,10 +42,11 @@ class Allocation:
         self.killed = False
         self.exit_codes: Dict[str, int] = {}
         self.start_time = time.time()
-        # current all-gather round: request_uuid -> (order key, data); result once complete
+        # all-gather rounds: the forming round (request_uuid -> (order key, data)) and the results
+        # + member uuids of the last completed rounds (a repeat post is an idempotent re-fetch)
         self.gather: Dict[str, Tuple[Any, Any]] = {}
-        self.gather_result: Optional[List[Any]] = None
-        self.gather_fetched: set = set()
+        self.gather_round = 0
+        self.gather_done: Dict[int, Tuple[List[Any], frozenset]] = {}
 
     def to_dict(self) -> Dict[str, Any]:
         return {"allocation_id": self.id, "task_id": self.task_id, "slots": self.slots, "state": self.state,
@@ -144,6 +145,9 @@ class Master:
         self.stream_cv = threading.Condition()
         self.stream_events: "collections.deque" = collections.deque(maxlen=capacity)
         self.stream_seq = 0
+        # per-process epoch: a client that echoes another process's epoch (the master restarted and
+        # its sequence started over) is told to resync whatever its `since`
+        self.stream_epoch = uuid.uuid4().hex[:12]
 
         def on_change(table: str, key: Any, cols: Dict[str, Any]) -> None:
             from determined_amd.master._db import STREAMED
@@ -159,16 +163,22 @@ class Master:
 
         self.db.on_change = on_change
 
-    def stream(self, since: int, timeout: float = 0.0, entities: Optional[List[str]] = None) -> Dict[str, Any]:
+    def stream(self, since: int, timeout: float = 0.0, entities: Optional[List[str]] = None,
+               epoch: Optional[str] = None) -> Dict[str, Any]:
+        """Events after ``since``; ``resync=True`` when the client cannot catch up incrementally:
+        the ring dropped what it missed, its ``since`` is ahead of this process's sequence, or it
+        echoes the ``epoch`` of an earlier master process."""
         deadline = time.time() + timeout
         with self.stream_cv:
             while True:
+                head = {"last_seq": self.stream_seq, "epoch": self.stream_epoch}
                 oldest = self.stream_events[0]["seq"] if self.stream_events else self.stream_seq + 1
-                if since + 1 < oldest and since < self.stream_seq:
-                    return {"events": [], "last_seq": self.stream_seq, "resync": True}
+                if ((since + 1 < oldest and since < self.stream_seq) or since > self.stream_seq
+                        or (epoch and epoch != self.stream_epoch)):
+                    return {"events": [], "resync": True, **head}
                 evs = [e for e in self.stream_events if e["seq"] > since and (not entities or e["entity"] in entities)]
                 if evs or time.time() >= deadline or self._closed:
-                    return {"events": evs, "last_seq": self.stream_seq, "resync": False}
+                    return {"events": evs, "resync": False, **head}
                 self.stream_cv.wait(max(0.0, min(1.0, deadline - time.time())))
 
     def _tick_loop(self) -> None:
@@ -917,25 +927,26 @@ class Master:
             a = self.allocations.get(alloc_id)
             if a is None:
                 raise KeyError(f"allocation {alloc_id} not found")
-            if a.gather_result is not None and (request_uuid in a.gather_fetched
-                                                or len(a.gather_fetched) >= len(a.gather_result)):
-                a.gather_result, a.gather_fetched = None, set()  # a peer starting the next round
-            if a.gather_result is None:
-                a.gather[request_uuid] = (rank if rank is not None else len(a.gather), data)
-                if len(a.gather) >= num_peers:
-                    a.gather_result = [d for _, d in sorted(a.gather.values(), key=lambda kv: kv[0])]
-                    a.gather = {}
-                    self.cv.notify_all()
-            while a.gather_result is None and time.time() < deadline and not self._closed:
+            for res, members in a.gather_done.values():
+                if request_uuid in members:  # a retried post of a finished round (lost response)
+                    return list(res)
+            my_round = a.gather_round
+            a.gather[request_uuid] = (rank if rank is not None else len(a.gather), data)
+            if len(a.gather) >= num_peers:
+                res = [d for _, d in sorted(a.gather.values(), key=lambda kv: kv[0])]
+                a.gather_done[my_round] = (res, frozenset(a.gather))
+                a.gather_done.pop(my_round - 4, None)  # keep the last few rounds for late re-fetches
+                a.gather, a.gather_round = {}, my_round + 1
+                self.cv.notify_all()
+            while my_round not in a.gather_done and time.time() < deadline and not self._closed:
                 if a.state == "TERMINATED":
                     raise RuntimeError(f"allocation {alloc_id} terminated during all-gather")
                 self.cv.wait(max(0.0, min(1.0, deadline - time.time())))
-            if a.gather_result is None:
-                a.gather.pop(request_uuid, None)
+            if my_round not in a.gather_done:
+                if a.gather_round == my_round:
+                    a.gather.pop(request_uuid, None)
                 raise TimeoutError(f"all-gather of allocation {alloc_id} timed out")
-            out = list(a.gather_result)
-            a.gather_fetched.add(request_uuid)
-            return out
+            return list(a.gather_done[my_round][0])
 
     def ack_preemption(self, alloc_id: str) -> None:
         with self.lock:

@@ -343,7 +343,8 @@ def build_routes(m: Master) -> List[Route]:
     @route("GET", "/api/v1/stream")
     def stream(q, b):
         ents = [e for e in q.get("entities", "").split(",") if e]
-        return m.stream(int(q.get("since", 0)), min(float(q.get("timeout_seconds", 0)), 60.0), ents or None)
+        return m.stream(int(q.get("since", 0)), min(float(q.get("timeout_seconds", 0)), 60.0), ents or None,
+                        q.get("epoch") or None)
 
     @route("GET", "/api/v1/allocations")
     def allocs(q, b):

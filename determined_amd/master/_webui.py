@@ -30,7 +30,7 @@ button{font-size:12px;margin-right:4px}pre{background:#0f1419;color:#d6deeb;padd
 <script>
 const $ = s => document.querySelector(s);
 let token = localStorage.getItem("det_token") || "";
-let seq = 0;
+let seq = 0, epoch = "";
 async function api(path, opts = {}) {
   const h = {"Content-Type": "application/json"};
   if (token) h["Authorization"] = "Bearer " + token;
@@ -154,9 +154,9 @@ async function route() {
 async function follow() {  // live updates: long-poll the master's event stream
   for (;;) {
     try {
-      const d = await api(`/api/v1/stream?since=${seq}&timeout_seconds=25`);
+      const d = await api(`/api/v1/stream?since=${seq}&timeout_seconds=25&epoch=${epoch}`);
       const changed = d.resync || d.events.length > 0;
-      seq = d.last_seq;
+      seq = d.last_seq; epoch = d.epoch || "";
       if (changed) await route();
     } catch (e) { await new Promise(r => setTimeout(r, 3000)); }
   }

@@ -61,6 +61,25 @@ def fusion_enabled(name: str) -> bool:
     return name not in _DISABLED
 
 
+def conv_health_check(device=None) -> None:
+    """Raise if any stream-K convolution on ``device`` timed out waiting for a partial tile
+    (conv_igemm.hip sk_gather: such a tile is written as NaN, never silently wrong).  Syncs the
+    device; called after conv tuning and at the trainer's reporting boundaries.  On a time-out the
+    flag buffers are reset and the stream-K configs are excluded from later tuning choices."""
+    import torch
+
+    if _ext is None or not torch.cuda.is_available():
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    n = int(_ext.conv_sk_timeouts(torch.empty(0, device=dev), True))
+    if n:
+        from determined_amd.ops import conv as _conv
+
+        _conv.exclude_stream_k()
+        raise RuntimeError(f"{n} stream-K convolution hand-off(s) timed out on {dev}: the affected output tiles "
+                           "were written as NaN; stream-K configs are now excluded from the tuning choices")
+
+
 from determined_amd.ops.optim import FusedAdamW, FusedSGD, fused_clip_grad_norm_  # noqa: E402
 from determined_amd.ops.norm import (  # noqa: E402
     FusedLayerNorm,
@@ -73,6 +92,7 @@ from determined_amd.ops.bn import BatchNormAct2d  # noqa: E402
 
 __all__ = [
     "available",
+    "conv_health_check",
     "ext",
     "FusedAdamW",
     "FusedSGD",

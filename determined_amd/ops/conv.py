@@ -116,6 +116,19 @@ def _allowed(kind: str, cfg: object) -> bool:
     return (kind, cfg) not in _EXCLUDE and ("*", cfg) not in _EXCLUDE
 
 
+def exclude_stream_k() -> None:
+    """Drop every stream-K tile config from the candidates (and forget choices that picked one):
+    called by ``ops.conv_health_check`` after a stream-K hand-off timed out."""
+    global _EXCLUDE
+    from determined_amd import ops
+
+    e = ops.ext()
+    sk = [c for c in range(e.conv_num_cfgs()) if e.conv_sk_cfg(c)]
+    _EXCLUDE = _EXCLUDE | frozenset(("*", c) for c in sk)
+    for k in [k for k, v in _TUNE.items() if isinstance(v, int) and not isinstance(v, bool) and v in sk]:
+        del _TUNE[k]
+
+
 def _prologue_pays(key: tuple, t_fused: Callable[[], float], t_plain: Callable[[], float]) -> bool:
     """Whether a BN apply fused into a conv's operand staging beats the separate apply pass plus
     the conv's best plain config for this layer (timed once, like the tile choice).  The 1x1
@@ -191,6 +204,8 @@ def save_tune_db(path: str) -> int:
 
 def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> object:
     global _DB_LOADED
+    from determined_amd import ops
+
     if not _DB_LOADED:
         _DB_LOADED = True
         load_tune_db()
@@ -205,6 +220,8 @@ def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> obj
     else:
         times = {c: _time_once(fn) for c, fn in cands.items()}
         choice = min(times, key=times.get)
+        if any(isinstance(c, int) and ops.ext().conv_sk_cfg(c) for c in cands):
+            ops.conv_health_check()  # every candidate ran several times: a hand-off time-out shows here
     _TUNE[key] = choice
     return choice
 
@@ -673,7 +690,11 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
         rm, rv, momentum = bn.train_step_args()
         st, pad = conv.stride[0], conv.padding[0]
         w = conv.weight
-        lazy = bool(lazy_grad) and ops.fusion_enabled("bn_lazy_bwd")
+        # Only a producer node that takes the parked entry (_LazyBNGrad.take) may receive the
+        # placeholder: if the previous conv fell back to its module (a hook / parametrization on
+        # it), its backward would read the unwritten placeholder as dY.
+        lazy = (bool(lazy_grad) and ops.fusion_enabled("bn_lazy_bwd") and y.requires_grad
+                and isinstance(y.grad_fn, (_BNActConvFn._backward_cls, _IGemmConvFn._backward_cls)))
         pro_cfgs = ([c for c in range(e.conv_num_cfgs()) if e.conv_pro_supported(y, w, c) and _allowed("fwd_pro", c)]
                     if stats_part is not None and ops.fusion_enabled("bn_prologue") and st == 1
                     and 2 * pad == w.shape[2] - 1

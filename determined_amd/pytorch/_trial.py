@@ -467,6 +467,10 @@ class _PyTorchTrialController:
         while self._steps_until_complete(length) > 0:
             per_batch = self._train_with_boundaries(self.training_enumerator, boundaries)
             m = self._aggregate_training_metrics(per_batch)
+            if self.context.device.type == "cuda":
+                from determined_amd import ops
+
+                ops.conv_health_check(self.context.device)  # stream-K conv hand-off time-outs raise here
             if self.is_chief and m["avg_metrics"]:
                 self.core_context.train.report_training_metrics(self.state.batches_trained, m["avg_metrics"],
                                                                 m["batch_metrics"])

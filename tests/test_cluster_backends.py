@@ -209,9 +209,10 @@ def test_master_allocation_all_gather():
         aid = f"{tid}.1"
         out = {}
 
-        def peer(r):
+        def peer(r, rnd=0):
             out[r] = s.post(f"/api/v1/allocations/{aid}/all_gather",
-                            {"request_uuid": f"u{r}", "num_peers": 3, "rank": r, "data": f"10.0.0.{r}"})["data"]
+                            {"request_uuid": f"u{r}-{rnd}", "num_peers": 3, "rank": r,
+                             "data": f"10.{rnd}.0.{r}"})["data"]
 
         ts = [threading.Thread(target=peer, args=(r,)) for r in (2, 0, 1)]
         for t in ts:
@@ -219,13 +220,22 @@ def test_master_allocation_all_gather():
         for t in ts:
             t.join(30)
         assert out == {r: ["10.0.0.0", "10.0.0.1", "10.0.0.2"] for r in range(3)}
-        # a second round on the same allocation starts fresh
-        ts = [threading.Thread(target=peer, args=(r,)) for r in range(3)]
+        # a retried post of a finished round (its response lost) re-fetches that round's result
+        # at once and does not disturb the next round, which is forming meanwhile
+        t1 = threading.Thread(target=peer, args=(1, 1))
+        t1.start()
+        time.sleep(0.3)
+        again = s.post(f"/api/v1/allocations/{aid}/all_gather",
+                       {"request_uuid": "u0-0", "num_peers": 3, "rank": 0, "data": "10.0.0.0",
+                        "timeout_seconds": 2})["data"]
+        assert again == ["10.0.0.0", "10.0.0.1", "10.0.0.2"]
+        # the second round on the same allocation fills with new uuids
+        ts = [threading.Thread(target=peer, args=(r, 1)) for r in (0, 2)]
         for t in ts:
             t.start()
-        for t in ts:
+        for t in ts + [t1]:
             t.join(30)
-        assert out[0] == ["10.0.0.0", "10.0.0.1", "10.0.0.2"]
+        assert out == {r: ["10.1.0.0", "10.1.0.1", "10.1.0.2"] for r in range(3)}
         with pytest.raises(Exception):
             s.post(f"/api/v1/allocations/{aid}/all_gather", {"request_uuid": "x", "num_peers": 2, "data": 1,
                                                               "timeout_seconds": 0.5})
@@ -426,3 +436,22 @@ def test_hpc_config_sections_validate():
                                                       pbs={"pbsbatch_args": "nope"})))
     assert any("slurm.bogus" in e for e in errs) and any("slurm.slots_per_node" in e for e in errs)
     assert any("pbs.pbsbatch_args" in e for e in errs)
+
+
+def test_slurm_exit_code_after_squeue_purged_the_job(tmp_path, monkeypatch):
+    """Slurm forgets finished jobs after MinJobAge: squeue then fails with 'Invalid job id'; the
+    exit file (or accounting) still gives the task's exit code instead of crashing the poll."""
+    from determined_amd.agent import backends
+
+    def fake_run(argv, timeout=60.0):
+        if argv[0] == "squeue":
+            raise RuntimeError("squeue -h -j 7 -o %T failed (1): slurm_load_jobs error: Invalid job id specified")
+        if argv[0] == "sacct":
+            return ""
+        raise AssertionError(argv)
+
+    monkeypatch.setattr(backends, "_run", fake_run)
+    b = backends.SlurmBackend()
+    assert b.exit_code("7", tmp_path) == 1  # purged, no exit file, no accounting: failed
+    (tmp_path / backends.EXIT_FILE).write_text("3\n")
+    assert b.exit_code("7", tmp_path) == 3

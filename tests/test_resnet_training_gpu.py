@@ -60,3 +60,59 @@ def test_resnet50_fused_training_follows_unfused_curve(monkeypatch):
     # deterministic kernels: the fused run repeats itself (a race shows up as run-to-run noise)
     for i, (a, b) in enumerate(zip(fused, fused2)):
         assert abs(a - b) <= 1e-2 * abs(b), (i, fused, fused2)  # MIOpen atomics: not bitwise
+
+
+def _grads(model, x, y):
+    loss = F.cross_entropy(model(x).float(), y)
+    loss.backward()
+    out = {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    return out
+
+
+def test_resnet50_hooked_inner_conv_falls_back_safely(monkeypatch):
+    """A forward hook on an inner conv makes that conv run through its module (not the fused
+    node); the BN after it must then not defer its backward apply into that conv (the module's
+    backward would read the unwritten placeholder): gradients match the all-fusions-off run."""
+    import determined_amd.ops as ops
+    from determined_amd.models.resnet import resnet50
+
+    ops.ext()
+    torch.manual_seed(0)
+    # no zero-init of the residual BNs: every conv gets a non-zero gradient at step 0
+    model = resnet50(num_classes=100, zero_init_residual=False).cuda().to(torch.bfloat16)
+    model = model.to(memory_format=torch.channels_last)
+    # conv2 (3x3) and conv3 (1x1) of stride-1 blocks: both normally take the next BN's deferred apply
+    hooks = [model.layer1[1].conv2.register_forward_hook(lambda m, i, o: None),
+             model.layer3[2].conv3.register_forward_hook(lambda m, i, o: None)]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    x = torch.randn(16, 3, 128, 128, generator=g, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (16,), generator=g, device="cuda")
+    # placeholders hold NaN: any consumer that reads one as data poisons the gradients
+    from determined_amd.ops import conv as conv_mod
+
+    for cls in (conv_mod._LazyBNGrad, conv_mod._StridedGrad):
+        orig = cls.park.__func__
+
+        def park(c, *a, _orig=orig):
+            ph = _orig(c, *a)
+            ph.fill_(float("nan"))
+            return ph
+        monkeypatch.setattr(cls, "park", classmethod(park))
+    monkeypatch.setattr(ops, "_DISABLED", frozenset())
+    fused = _grads(model, x, y)
+    fused2 = _grads(model, x, y)
+    monkeypatch.setattr(ops, "_DISABLED", ALL_FUSIONS)
+    plain = _grads(model, x, y)
+    for h in hooks:
+        h.remove()
+    assert fused.keys() == plain.keys()
+    for n in plain:
+        a, b = fused[n], plain[n]
+        assert torch.isfinite(a).all(), n
+        cos = F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+        assert cos > 0.98, (n, cos)
+        cos2 = F.cosine_similarity(a.flatten(), fused2[n].flatten(), dim=0).item()
+        assert cos2 > 0.999, (n, cos2)  # no uninitialised memory read: the run repeats itself

@@ -55,6 +55,12 @@ def test_stream_long_poll_delivers_entity_changes(master):
     for i in range(m.stream_events.maxlen + 5):
         m.db.update("tasks", "id", "nope", state="X")
     assert s.get("/api/v1/stream", params={"since": 1})["resync"] is True
+    # a cursor from an earlier master process: ahead of this sequence, or another epoch
+    cur = s.get("/api/v1/stream", params={"since": m.stream_seq})
+    assert cur["resync"] is False and cur["epoch"] == m.stream_epoch
+    assert s.get("/api/v1/stream", params={"since": m.stream_seq + 100})["resync"] is True
+    assert s.get("/api/v1/stream", params={"since": m.stream_seq, "epoch": "old-process"})["resync"] is True
+    assert s.get("/api/v1/stream", params={"since": m.stream_seq, "epoch": cur["epoch"]})["resync"] is False
 
 
 @pytest.mark.skipif(__import__("shutil").which("node") is None, reason="node not installed")
