@@ -31,6 +31,7 @@ class DeviceGradScaler:
         self._growth_tracker: Optional[torch.Tensor] = None
         self._found_inf: Optional[torch.Tensor] = None
         self._inv_scale: Optional[torch.Tensor] = None
+        self._unscaled: set = set()  # ids of optimizers unscale_()d since the last update()
 
     def is_enabled(self) -> bool:
         return self._enabled
@@ -53,16 +54,37 @@ class DeviceGradScaler:
     def get_scale(self) -> float:
         return float(self._scale.item()) if self._scale is not None else self._init_scale
 
+    def unscale_(self, optimizer: torch.optim.Optimizer) -> None:
+        """Divide the optimizer's gradients by the scale now (before gradient clipping) and record
+        non-finite values; the following :meth:`step` then only applies the skip decision."""
+        if not self._enabled or self._scale is None:
+            return
+        assert self._inv_scale is not None and self._found_inf is not None
+        if id(optimizer) in self._unscaled:
+            raise RuntimeError("unscale_() has already been called on this optimizer since the last update()")
+        torch.reciprocal(self._scale, out=self._inv_scale)
+        found = torch.zeros((1,), dtype=torch.float32, device=self._scale.device)
+        grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+        if grads:
+            torch._amp_foreach_non_finite_check_and_unscale_(grads, found, self._inv_scale)
+        self._found_inf.copy_(torch.maximum(self._found_inf, found.to(torch.int32)))
+        self._unscaled.add(id(optimizer))
+
     def step(self, optimizer: torch.optim.Optimizer, *args: Any, **kwargs: Any) -> Optional[float]:
         if not self._enabled:
             return optimizer.step(*args, **kwargs)
         from determined_amd.ops.optim import _FusedBase
 
         assert self._scale is not None and self._inv_scale is not None and self._found_inf is not None
+        fused = isinstance(optimizer, _FusedBase) and any(p.is_cuda for g in optimizer.param_groups for p in g["params"])
+        if id(optimizer) in self._unscaled:  # gradients already unscaled and checked (unscale_)
+            if fused:  # the skip decision stays on the device
+                return optimizer.step(*args, found_inf=self._found_inf, **kwargs)
+            if int(self._found_inf.item()) == 0:
+                return optimizer.step(*args, **kwargs)
+            return None
         torch.reciprocal(self._scale, out=self._inv_scale)
-        if isinstance(optimizer, _FusedBase) and any(
-            p.is_cuda for g in optimizer.param_groups for p in g["params"]
-        ):
+        if fused:
             self._found_inf.zero_()
             return optimizer.step(*args, grad_scale=self._inv_scale, found_inf=self._found_inf,
                                   check_finite=True, **kwargs)
@@ -79,6 +101,7 @@ class DeviceGradScaler:
     def update(self, new_scale: Optional[float] = None) -> None:
         if not self._enabled or self._scale is None:
             return
+        self._unscaled.clear()
         if new_scale is not None:
             self._scale.fill_(float(new_scale))
             return
@@ -91,6 +114,7 @@ class DeviceGradScaler:
             self._backoff_factor,
             self._growth_interval,
         )
+        self._found_inf.zero_()  # unscale_() accumulates into it until the next update()
 
     def state_dict(self) -> Dict[str, Any]:
         if not self._enabled:

@@ -6,6 +6,7 @@ from determined_amd.pytorch._callback import PyTorchCallback
 from determined_amd.pytorch._lr_scheduler import LRScheduler
 from determined_amd.pytorch._reducer import MetricReducer, Reducer, _PyTorchReducerContext, _SimpleReducer
 from determined_amd.pytorch._context import PyTorchTrialContext
+from determined_amd.pytorch._experimental import PyTorchExperimentalContext
 from determined_amd.pytorch._trial import (
     Batch,
     Epoch,

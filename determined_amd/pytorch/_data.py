@@ -82,6 +82,16 @@ class DataLoader:
         return len(self._base_batch_sampler(0))
 
 
+def dataset_repro_message(name: str, obj: Any) -> str:
+    """The controller's error for a loader that is not a :class:`DataLoader` (reference
+    ``pytorch._dataset_repro_warning``)."""
+    return (f"{name}() returned a {type(obj).__name__}, not a determined_amd.pytorch.DataLoader, whose samplers "
+            "make shuffling reproducible, resume at the right batch after a pause and shard the data across "
+            "slots.  Return a determined_amd.pytorch.DataLoader, or call "
+            "context.experimental.disable_dataset_reproducibility_checks() in the trial's __init__ to use any "
+            "loader (reproducibility and sharding are then the loader's job).")
+
+
 def adapt_batch_sampler(batch_sampler: Any, repeat: bool = False, skip: int = 0, num_replicas: int = 1,
                         rank: int = 0) -> Any:
     if num_replicas > 1:

@@ -231,6 +231,8 @@ class _PyTorchTrialController:
             self.training_loader = tl.get_data_loader(repeat=True, skip=skip, num_replicas=dist.size,
                                                       rank=dist.rank, seed=self.context.get_trial_seed())
         else:
+            if not self.context.experimental._data_repro_checks_disabled:
+                raise RuntimeError(_data.dataset_repro_message("build_training_data_loader", tl))
             self._train_loader_len = len(tl)
             self.training_loader = _repeat(tl, skip)
         self.context._epoch_len = max(self._train_loader_len, 1)
@@ -241,6 +243,8 @@ class _PyTorchTrialController:
                                                         shard_batches=True)
             self._val_shard = (1, 0)
         else:
+            if not self.context.experimental._data_repro_checks_disabled:
+                raise RuntimeError(_data.dataset_repro_message("build_validation_data_loader", vl))
             self.validation_loader = vl
             self._val_shard = (1, 0)
 
@@ -254,7 +258,8 @@ class _PyTorchTrialController:
         for idx, batch in enumerate(self.validation_loader):
             if idx % n_shards != shard:
                 continue
-            batch = self.context.to_device(batch)
+            if self.context.experimental._auto_to_device:
+                batch = self.context.to_device(batch)
             yield self.trial.evaluate_batch(batch=batch, batch_idx=idx)
 
     # -- checkpointing -----------------------------------------------------------------------
@@ -381,15 +386,16 @@ class _PyTorchTrialController:
                         s.step()
 
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
-        batch = self.context.to_device(batch)
+        if self.context.experimental._auto_to_device:
+            batch = self.context.to_device(batch)
         with contextlib.ExitStack() as st:
             if self.context.profiler is not None:
                 st.enter_context(self.context.profiler)
             out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
             if self.context.profiler is not None:
                 self.context.profiler.step()
-        if self.context._scaler is not None and self.context._should_communicate_and_update() and \
-                hasattr(self.context._scaler, "update"):
+        if self.context._scaler is not None and self.context.experimental._auto_amp and \
+                self.context._should_communicate_and_update():
             self.context._scaler.update()
         if isinstance(out, torch.Tensor):
             out = {"loss": out}

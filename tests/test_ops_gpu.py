@@ -144,6 +144,36 @@ def test_scaler_skips_on_inf_without_sync(ops):
     assert scaler.get_scale() == 1024.0
 
 
+def test_scaler_unscale_then_clip_then_step(ops):
+    """use_amp's order: unscale_ before clipping, then step applies only the skip decision."""
+    ref = _params([(1000,), (33,)], seed=9)
+    ps = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    for a, b in zip(ps, ref):
+        a.grad = b.grad * 256.0  # gradients of a loss scaled by 256
+    torch.nn.utils.clip_grad_norm_(ref, 0.5)
+    torch.optim.SGD(ref, lr=0.1).step()
+    opt = ops.FusedSGD(ps, lr=0.1)
+    scaler = ops.DeviceGradScaler(init_scale=256.0)
+    scaler.scale(torch.zeros((), device="cuda"))
+    scaler.unscale_(opt)
+    with pytest.raises(RuntimeError):
+        scaler.unscale_(opt)
+    torch.nn.utils.clip_grad_norm_(ps, 0.5)
+    scaler.step(opt)
+    scaler.update()
+    for a, b in zip(ps, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    # a non-finite gradient seen by unscale_ skips the step
+    before = [p.detach().clone() for p in ps]
+    ps[1].grad.fill_(float("nan"))
+    scaler.unscale_(opt)
+    scaler.step(opt)
+    scaler.update()
+    for p, b in zip(ps, before):
+        torch.testing.assert_close(p.detach(), b)
+    assert scaler.get_scale() == 128.0
+
+
 def _ref_ln(x, w, b, eps, rms):
     xf = x.float()
     if rms:

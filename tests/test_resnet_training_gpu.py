@@ -73,25 +73,36 @@ def _grads(model, x, y):
 def test_resnet50_hooked_inner_conv_falls_back_safely(monkeypatch):
     """A forward hook on an inner conv makes that conv run through its module (not the fused
     node); the BN after it must then not defer its backward apply into that conv (the module's
-    backward would read the unwritten placeholder): gradients match the all-fusions-off run."""
+    backward would read the unwritten placeholder).  Placeholders are NaN-filled here, so any read
+    shows as a non-finite gradient; the gradients must also agree with an fp32 run of the same
+    weights as well as the all-fusions-off bf16 run does (bf16 BN-parameter gradients of a deep
+    ResNet are noisy on either path: scripts/dev/grad_parity.py)."""
     import determined_amd.ops as ops
     from determined_amd.models.resnet import resnet50
+    from determined_amd.ops import conv as conv_mod
 
     ops.ext()
     torch.manual_seed(0)
-    # no zero-init of the residual BNs: every conv gets a non-zero gradient at step 0
-    model = resnet50(num_classes=100, zero_init_residual=False).cuda().to(torch.bfloat16)
-    model = model.to(memory_format=torch.channels_last)
-    # conv2 (3x3) and conv3 (1x1) of stride-1 blocks: both normally take the next BN's deferred apply
-    hooks = [model.layer1[1].conv2.register_forward_hook(lambda m, i, o: None),
-             model.layer3[2].conv3.register_forward_hook(lambda m, i, o: None)]
+    # residual BNs at a small scale instead of torchvision's zero init: every conv gets a
+    # non-zero gradient at step 0 and the fp32 comparison stays well-conditioned
+    model = resnet50(num_classes=100)
+    for blk in (b for layer in (model.layer1, model.layer2, model.layer3, model.layer4) for b in layer):
+        torch.nn.init.constant_(blk.bn3.weight, 0.2)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
-    x = torch.randn(16, 3, 128, 128, generator=g, device="cuda").to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 128, 128, generator=g, device="cuda")
     y = torch.randint(0, 100, (16,), generator=g, device="cuda")
-    # placeholders hold NaN: any consumer that reads one as data poisons the gradients
-    from determined_amd.ops import conv as conv_mod
+
+    def grads(dtype, disabled):
+        monkeypatch.setattr(ops, "_DISABLED", disabled)
+        m = resnet50(num_classes=100)
+        m.load_state_dict(sd)
+        m = m.cuda().to(dtype).to(memory_format=torch.channels_last)
+        # conv2 (3x3) and conv3 (1x1) of stride-1 blocks: both normally take the next BN's deferred apply
+        m.layer1[1].conv2.register_forward_hook(lambda mod, i, o: None)
+        m.layer3[2].conv3.register_forward_hook(lambda mod, i, o: None)
+        return _grads(m, x.to(dtype).contiguous(memory_format=torch.channels_last), y)
 
     for cls in (conv_mod._LazyBNGrad, conv_mod._StridedGrad):
         orig = cls.park.__func__
@@ -101,18 +112,15 @@ def test_resnet50_hooked_inner_conv_falls_back_safely(monkeypatch):
             ph.fill_(float("nan"))
             return ph
         monkeypatch.setattr(cls, "park", classmethod(park))
-    monkeypatch.setattr(ops, "_DISABLED", frozenset())
-    fused = _grads(model, x, y)
-    fused2 = _grads(model, x, y)
-    monkeypatch.setattr(ops, "_DISABLED", ALL_FUSIONS)
-    plain = _grads(model, x, y)
-    for h in hooks:
-        h.remove()
-    assert fused.keys() == plain.keys()
-    for n in plain:
-        a, b = fused[n], plain[n]
-        assert torch.isfinite(a).all(), n
-        cos = F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
-        assert cos > 0.98, (n, cos)
-        cos2 = F.cosine_similarity(a.flatten(), fused2[n].flatten(), dim=0).item()
-        assert cos2 > 0.999, (n, cos2)  # no uninitialised memory read: the run repeats itself
+    ref = grads(torch.float32, ALL_FUSIONS)
+    fused = grads(torch.bfloat16, frozenset())
+    plain = grads(torch.bfloat16, ALL_FUSIONS)
+    assert fused.keys() == plain.keys() == ref.keys()
+    bad = []
+    for n in ref:
+        assert torch.isfinite(fused[n]).all(), n  # no placeholder was read
+        cf = F.cosine_similarity(fused[n].flatten(), ref[n].flatten(), dim=0).item()
+        cp = F.cosine_similarity(plain[n].flatten(), ref[n].flatten(), dim=0).item()
+        if cf < cp - 0.05 or cf < 0.7:
+            bad.append((n, round(cf, 4), round(cp, 4)))
+    assert not bad, bad

@@ -149,3 +149,117 @@ def test_overwrite_deepspeed_config(tmp_path):
     p.write_text('{"a": 1, "a": 2}')
     with pytest.raises(ValueError):
         overwrite_deepspeed_config(str(p), {})
+
+
+# ------------------------------------------------------------------ context.experimental
+def _tiny_trial_cls(mode: str):
+    """A regression trial exercising ``context.experimental`` (reference ``_experimental.py``)."""
+    import torch.nn.functional as F
+
+    from determined_amd import pytorch
+
+    class DS(torch.utils.data.Dataset):
+        def __init__(self, n):
+            g = torch.Generator().manual_seed(0)
+            self.x = torch.randn(n, 8, generator=g)
+            self.y = self.x.sum(1, keepdim=True)
+
+        def __len__(self):
+            return len(self.x)
+
+        def __getitem__(self, i):
+            return self.x[i], self.y[i]
+
+    class T(pytorch.PyTorchTrial):
+        def __init__(self, context):
+            self.context = context
+            self.seen_devices = []
+            if mode == "amp":
+                context.experimental.use_amp()
+            if mode in ("plain_loader", "no_to_device"):
+                context.experimental.disable_dataset_reproducibility_checks()
+            if mode == "no_to_device":
+                context.experimental.disable_auto_to_device()
+            self.model = context.wrap_model(torch.nn.Linear(8, 1))
+            self.opt = context.wrap_optimizer(torch.optim.SGD(self.model.parameters(), lr=0.05))
+
+        def train_batch(self, batch, epoch_idx, batch_idx):
+            x, y = batch
+            self.seen_devices.append(type(x).__name__)
+            out = self.model(x)
+            if mode == "amp":
+                assert out.dtype == torch.bfloat16  # the wrapped forward runs under autocast (CPU: bf16)
+            loss = F.mse_loss(out.float(), y)
+            self.context.backward(loss)
+            self.context.step_optimizer(self.opt, clip_grads=lambda ps: torch.nn.utils.clip_grad_norm_(ps, 10.0))
+            return {"loss": loss}
+
+        def evaluate_batch(self, batch, batch_idx):
+            x, y = batch
+            return {"validation_loss": F.mse_loss(self.model(x).float(), y)}
+
+        def build_training_data_loader(self):
+            if mode in ("plain_loader", "no_to_device", "repro_error"):
+                return torch.utils.data.DataLoader(DS(64), batch_size=8)
+            return pytorch.DataLoader(DS(64), batch_size=8)
+
+        def build_validation_data_loader(self):
+            return pytorch.DataLoader(DS(16), batch_size=8)
+
+    return T
+
+
+@pytest.mark.parametrize("mode", ["amp", "plain_loader", "no_to_device"])
+def test_experimental_context_switches(mode):
+    from determined_amd import pytorch
+
+    T = _tiny_trial_cls(mode)
+    with tempfile.TemporaryDirectory() as d:
+        with pytorch.init(hparams={"global_batch_size": 8}, exp_conf={"data": {}}, checkpoint_storage=d) as ctx:
+            trial = T(ctx)
+            assert isinstance(ctx.experimental, pytorch.PyTorchExperimentalContext)
+            pytorch.Trainer(trial, ctx).fit(max_length=pytorch.Batch(4), validation_period=pytorch.Batch(4))
+        assert len(trial.seen_devices) == 4
+        if mode == "amp":
+            assert ctx.experimental._auto_amp and ctx._scaler is not None
+
+
+def test_plain_torch_loader_needs_the_repro_switch():
+    from determined_amd import pytorch
+
+    T = _tiny_trial_cls("repro_error")
+    with tempfile.TemporaryDirectory() as d:
+        with pytest.raises(RuntimeError, match="disable_dataset_reproducibility_checks"):
+            with pytorch.init(hparams={"global_batch_size": 8}, exp_conf={"data": {}}, checkpoint_storage=d) as ctx:
+                pytorch.Trainer(T(ctx), ctx).fit(max_length=pytorch.Batch(2))
+
+
+def test_manual_scaler_is_not_applied_automatically():
+    """Reference semantics: a scaler passed to ``wrap_scaler`` (without ``use_amp``) is the trial's
+    to apply -- ``backward`` does not scale the loss and ``step_optimizer`` steps through it only
+    when passed ``scaler=``."""
+    from determined_amd import pytorch
+    from determined_amd.ops.scaler import DeviceGradScaler
+
+    with tempfile.TemporaryDirectory() as d:
+        with pytorch.init(hparams={"global_batch_size": 8}, exp_conf={"data": {}}, checkpoint_storage=d) as ctx:
+            m = ctx.wrap_model(torch.nn.Linear(4, 1))
+            opt = ctx.wrap_optimizer(torch.optim.SGD(m.parameters(), lr=0.0))
+            calls = []
+
+            class Spy(DeviceGradScaler):
+                def scale(self, t):
+                    calls.append("scale")
+                    return t
+
+                def step(self, o, *a, **k):
+                    calls.append("step")
+                    return o.step()
+
+            s = ctx.wrap_scaler(Spy(enabled=False))
+            ctx.backward(m(torch.ones(2, 4)).sum())
+            ctx.step_optimizer(opt)
+            assert calls == []
+            ctx.backward(m(torch.ones(2, 4)).sum())
+            ctx.step_optimizer(opt, scaler=s)
+            assert calls == ["step"]
