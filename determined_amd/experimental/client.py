@@ -655,3 +655,203 @@ def stream_trials_validation_metrics(trial_ids: List[int]) -> Iterable[Dict[str,
 def iter_trials_metrics(trial_ids: List[int], group: str) -> Iterable[Dict[str, Any]]:
     for tid in trial_ids:
         yield from Trial(_s(), tid).iter_metrics(group)
+
+
+# ---------------------------------------------------------------------------------------------
+# users, workspaces, projects (reference: common/experimental/{user,workspace,project}.py and the
+# user / workspace functions of experimental/client.py)
+# ---------------------------------------------------------------------------------------------
+class User:
+    def __init__(self, session: Session, data: Dict[str, Any]) -> None:
+        self._session = session
+        self._data = data
+
+    @property
+    def user_id(self) -> int:
+        return int(self._data["id"])
+
+    @property
+    def username(self) -> str:
+        return self._data["username"]
+
+    @property
+    def display_name(self) -> str:
+        return self._data.get("display_name") or ""
+
+    @property
+    def admin(self) -> bool:
+        return bool(self._data.get("admin"))
+
+    @property
+    def active(self) -> bool:
+        return bool(self._data.get("active"))
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/users/{self.user_id}")["user"]
+
+    def _patch(self, **cols: Any) -> None:
+        self._data = self._session.patch(f"/api/v1/users/{self.user_id}", cols)["user"]
+
+    def rename(self, new_username: str) -> None:
+        self._patch(username=new_username)
+
+    def activate(self) -> None:
+        self._patch(active=True)
+
+    def deactivate(self) -> None:
+        self._patch(active=False)
+
+    def change_display_name(self, display_name: str) -> None:
+        self._patch(display_name=display_name)
+
+    def change_password(self, new_password: str) -> None:
+        self._data = self._session.post(f"/api/v1/users/{self.user_id}/password", {"password": new_password})["user"]
+
+    def __repr__(self) -> str:
+        return f"User(id={self.user_id}, username={self.username})"
+
+
+def create_user(username: str, admin: bool = False, password: Optional[str] = None,
+                display_name: Optional[str] = None) -> User:
+    r = _s().post("/api/v1/users", {"user": {"username": username, "admin": admin, "active": True,
+                                             "display_name": display_name or ""}, "password": password or ""})
+    return User(_s(), r["user"])
+
+
+def get_user_by_id(user_id: int) -> User:
+    return User(_s(), _s().get(f"/api/v1/users/{int(user_id)}")["user"])
+
+
+def get_user_by_name(user_name: str) -> User:
+    return User(_s(), _s().get(f"/api/v1/users/{user_name}")["user"])
+
+
+def whoami() -> User:
+    return User(_s(), _s().get("/api/v1/me")["user"])
+
+
+def get_session_username() -> str:
+    return whoami().username
+
+
+def list_users(active: Optional[bool] = None) -> List[User]:
+    rows = _s().get("/api/v1/users")["users"]
+    return [User(_s(), r) for r in rows if active is None or bool(r.get("active")) == active]
+
+
+class Project:
+    def __init__(self, session: Session, data: Dict[str, Any]) -> None:
+        self._session = session
+        self._data = data
+
+    @property
+    def id(self) -> int:
+        return int(self._data["id"])
+
+    @property
+    def name(self) -> str:
+        return self._data["name"]
+
+    @property
+    def description(self) -> str:
+        return self._data.get("description") or ""
+
+    @property
+    def workspace_id(self) -> int:
+        return int(self._data["workspace_id"])
+
+    @property
+    def archived(self) -> bool:
+        return bool(self._data.get("archived"))
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/projects/{self.id}")["project"]
+
+    def list_experiments(self) -> List["Experiment"]:
+        rows = self._session.get(f"/api/v1/projects/{self.id}/experiments")["experiments"]
+        return [Experiment(self._session, int(r["id"])) for r in rows]
+
+    def set_name(self, name: str) -> None:
+        self._data = self._session.patch(f"/api/v1/projects/{self.id}", {"name": name})["project"]
+
+    def set_description(self, description: str) -> None:
+        self._data = self._session.patch(f"/api/v1/projects/{self.id}", {"description": description})["project"]
+
+    def archive(self) -> None:
+        self._data = self._session.post(f"/api/v1/projects/{self.id}/archive", {})["project"]
+
+    def unarchive(self) -> None:
+        self._data = self._session.post(f"/api/v1/projects/{self.id}/unarchive", {})["project"]
+
+    def __repr__(self) -> str:
+        return f"Project(id={self.id}, name={self.name})"
+
+
+class Workspace:
+    def __init__(self, session: Session, data: Dict[str, Any]) -> None:
+        self._session = session
+        self._data = data
+
+    @property
+    def id(self) -> int:
+        return int(self._data["id"])
+
+    @property
+    def name(self) -> str:
+        return self._data["name"]
+
+    @property
+    def archived(self) -> bool:
+        return bool(self._data.get("archived"))
+
+    def reload(self) -> None:
+        self._data = self._session.get(f"/api/v1/workspaces/{self.id}")["workspace"]
+
+    def list_projects(self) -> List[Project]:
+        rows = self._session.get(f"/api/v1/workspaces/{self.id}/projects")["projects"]
+        return [Project(self._session, r) for r in rows]
+
+    def get_project(self, project_name: str) -> Project:
+        for p in self.list_projects():
+            if p.name == project_name:
+                return p
+        raise NotFoundException(404, f"project {project_name!r} not found in workspace {self.name!r}")
+
+    def create_project(self, name: str, description: Optional[str] = None) -> Project:
+        r = self._session.post(f"/api/v1/workspaces/{self.id}/projects",
+                               {"name": name, "description": description or ""})
+        return Project(self._session, r["project"])
+
+    def delete_project(self, name: str) -> None:
+        self._session.delete(f"/api/v1/projects/{self.get_project(name).id}")
+
+    def list_pools(self) -> List[Dict[str, Any]]:
+        """Resource pools usable from this workspace (every pool: pools are not bound to workspaces)."""
+        return list(self._session.get("/api/v1/resource-pools").get("resource_pools") or [])
+
+    def __repr__(self) -> str:
+        return f"Workspace(id={self.id}, name={self.name})"
+
+
+def get_workspace(name: str) -> Workspace:
+    return Workspace(_s(), _s().get(f"/api/v1/workspaces/{name}")["workspace"])
+
+
+def list_workspaces() -> List[Workspace]:
+    return [Workspace(_s(), r) for r in _s().get("/api/v1/workspaces")["workspaces"]]
+
+
+def create_workspace(name: str) -> Workspace:
+    return Workspace(_s(), _s().post("/api/v1/workspaces", {"name": name})["workspace"])
+
+
+def delete_workspace(name: str) -> None:
+    _s().delete(f"/api/v1/workspaces/{name}")
+
+
+def get_model_by_id(model_id: int) -> Model:
+    return get_model(int(model_id))
+
+
+def stream_trials_metrics(trial_ids: List[int], group: str) -> Iterable[Dict[str, Any]]:
+    return iter_trials_metrics(trial_ids, group)

@@ -229,6 +229,10 @@ class IAM:
         for k in ("display_name",):
             if k in body:
                 cols[k] = body[k]
+        if "username" in body and body["username"] != u["username"]:  # rename (admin only, above)
+            if not body["username"] or self.db.one("SELECT id FROM users WHERE username=?", [body["username"]]):
+                raise AuthError(400, f"username {body['username']!r} is empty or taken")
+            cols["username"] = body["username"]
         for k in ("admin", "active"):
             if k in body:
                 cols[k] = int(bool(body[k]))

@@ -159,3 +159,44 @@ def test_cli_login_workspace_project(rbac_master, tmp_path, monkeypatch, capsys)
     assert '"Editor"' in capsys.readouterr().out
     assert main(["-m", url, "user", "logout"]) == 0
     assert main(["-m", url, "user", "whoami"]) == 1
+
+
+def test_sdk_users_workspaces_projects(rbac_master):
+    """The SDK's user / workspace / project objects (reference ``experimental/client.py`` +
+    ``common/experimental/{user,workspace,project}.py``) over the RBAC master."""
+    from determined_amd.experimental import client
+
+    url, _ = rbac_master
+    client.login(url, user="admin", password="")
+    try:
+        assert client.whoami().username == "admin" and client.get_session_username() == "admin"
+        u = client.create_user("sdk-user", password="pw1", display_name="SDK")
+        assert client.get_user_by_name("sdk-user").user_id == u.user_id
+        assert client.get_user_by_id(u.user_id).display_name == "SDK"
+        u.change_display_name("Renamed")
+        u.rename("sdk-user2")
+        u.deactivate()
+        assert not client.get_user_by_id(u.user_id).active
+        assert "sdk-user2" in {x.username for x in client.list_users(active=False)}
+        u.activate()
+        u.change_password("pw2")
+        with pytest.raises(APIException):
+            _login(url, "sdk-user2", "pw1")
+        _login(url, "sdk-user2", "pw2")
+        w = client.create_workspace("sdk-ws")
+        assert client.get_workspace("sdk-ws").id == w.id
+        assert "sdk-ws" in {x.name for x in client.list_workspaces()}
+        p = w.create_project("sdk-proj", "first")
+        assert w.get_project("sdk-proj").id == p.id and p.description == "first"
+        p.set_description("second")
+        p.reload()
+        assert p.description == "second" and p.list_experiments() == []
+        p.archive()
+        assert p.archived
+        p.unarchive()
+        w.delete_project("sdk-proj")
+        assert w.list_projects() == []
+        client.delete_workspace("sdk-ws")
+        assert "sdk-ws" not in {x.name for x in client.list_workspaces()}
+    finally:
+        client.logout()
