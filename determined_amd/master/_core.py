@@ -95,21 +95,24 @@ class ExperimentRec:
 class Master:
     def __init__(self, db_path: str = ":memory:", policy: str = "priority", fit: str = "best",
                  preemption: bool = True, cluster_id: Optional[str] = None, master_url: str = "http://127.0.0.1:8080",
-                 auth_token: Optional[str] = None, auth: str = "none") -> None:
+                 auth_token: Optional[str] = None, auth: str = "none",
+                 resource_pools: Optional[List[Dict[str, Any]]] = None, default_compute_pool: Optional[str] = None,
+                 default_aux_pool: Optional[str] = None) -> None:
         from determined_amd._native import load
         from determined_amd.master._iam import IAM
+        from determined_amd.master._pools import PoolSet, parse_pools
 
         self.native = load()
         self.lock = threading.RLock()
         self.cv = threading.Condition(self.lock)
         self.db = DB(db_path)
         self.iam = IAM(self.db, mode=auth, cluster_token=auth_token)
-        pol = {"priority": self.native.Policy.PRIORITY, "fair_share": self.native.Policy.FAIR_SHARE,
-               "round_robin": self.native.Policy.ROUND_ROBIN}[policy]
         self.policy = policy
         self.fit = fit
-        self.sched = self.native.Scheduler(pol, self.native.Fit.BEST if fit == "best" else self.native.Fit.WORST,
-                                           preemption)
+        # one native scheduler per resource pool (master/_pools.py); a single "default" pool
+        # with the master-wide policy unless the config lists pools
+        self.sched = PoolSet(self.native, parse_pools(resource_pools, policy, fit, preemption),
+                             default_compute_pool, default_aux_pool)
         self.cluster_id = cluster_id or str(uuid.uuid4())
         self.master_url = master_url
         self.auth_token = auth_token
@@ -234,6 +237,9 @@ class Master:
                           parent_id: Optional[int] = None, unmanaged: bool = False) -> int:
         cfg = expconf.parse(cfg)
         with self.lock:
+            res = cfg["resources"]
+            res["resource_pool"] = self.check_pool(res.get("resource_pool"), int(res.get("slots_per_trial", 1)),
+                                                   cfg.get("workspace") or "Uncategorized")
             eid = self.db.insert("experiments", name=cfg["name"], state="ACTIVE" if activate else "PAUSED",
                                  config=cfg, model_def=model_def, parent_id=parent_id, start_time=time.time(),
                                  description=cfg.get("description") or "", labels=cfg.get("labels") or [],
@@ -536,12 +542,14 @@ class Master:
         prio = exp.config["resources"].get("priority")
         self.sched.add_request(aid, f"exp-{exp.id}", slots, int(prio) if prio is not None else 42,
                                float(exp.config["resources"].get("weight", 1)), self._next_order(), True,
-                               list(tr.excluded_agents))
+                               list(tr.excluded_agents), pool=exp.config["resources"].get("resource_pool") or None)
         self.cv.notify_all()
 
     def create_command(self, cmd: List[str], slots: int = 0, env: Optional[Dict[str, str]] = None,
-                       kind: str = "COMMAND", workdir_b64: Optional[str] = None) -> str:
+                       kind: str = "COMMAND", workdir_b64: Optional[str] = None,
+                       resource_pool: Optional[str] = None, priority: Optional[int] = None) -> str:
         with self.lock:
+            pool = self.check_pool(resource_pool, slots, None)
             task_id = f"{kind.lower()}-{uuid.uuid4().hex[:8]}"
             aid = f"{task_id}.1"
             a = Allocation(aid, task_id, slots, kind=kind)
@@ -549,11 +557,53 @@ class Master:
             a.env = env or {}  # type: ignore[attr-defined]
             a.workdir_b64 = workdir_b64  # type: ignore[attr-defined]
             self.allocations[aid] = a
-            self.db.insert("tasks", id=task_id, type=kind, state="PENDING", config={"cmd": cmd, "slots": slots},
+            self.db.insert("tasks", id=task_id, type=kind, state="PENDING",
+                           config={"cmd": cmd, "slots": slots, "resource_pool": pool,
+                                   "priority": 42 if priority is None else int(priority)},
                            start_time=time.time())
-            self.sched.add_request(aid, task_id, slots, 42, 1.0, self._next_order(), False)
+            self.sched.add_request(aid, task_id, slots, 42 if priority is None else int(priority), 1.0,
+                                   self._next_order(), False, pool=pool)
             self.cv.notify_all()
             return task_id
+
+    # ================================================================ resource pools
+    def check_pool(self, name: Optional[str], slots: int, workspace: Optional[str]) -> str:
+        """The pool a request lands in (named, or the compute / aux default by slots); a pool bound
+        to workspaces takes only their experiments (reference ``api_resourcepool.go`` bindings)."""
+        from determined_amd.master._pools import PoolError
+
+        try:
+            pool = self.sched.resolve(name, slots)
+        except PoolError as e:
+            raise ValueError(str(e))
+        if workspace is not None:
+            bound = self.pool_bindings(pool)
+            if bound:
+                w = self.db.one("SELECT id FROM workspaces WHERE name=?", [workspace])
+                if w is None or int(w["id"]) not in bound:
+                    raise ValueError(f"resource pool {pool!r} is bound to other workspaces than {workspace!r}")
+        return pool
+
+    def pool_bindings(self, pool: str) -> List[int]:
+        return [int(r["workspace_id"]) for r in self.db.all("SELECT workspace_id FROM pool_bindings WHERE pool=? "
+                                                             "ORDER BY workspace_id", [pool])]
+
+    def set_pool_bindings(self, pool: str, workspace_ids: List[int], mode: str) -> List[int]:
+        """``mode``: add / remove / replace the workspaces bound to ``pool``."""
+        if pool not in self.sched.pools:
+            raise KeyError(f"resource pool {pool!r} does not exist")
+        with self.lock:
+            cur = set(self.pool_bindings(pool))
+            ids = {int(w) for w in workspace_ids}
+            new = cur | ids if mode == "add" else (cur - ids if mode == "remove" else ids)
+            self.db.execute("DELETE FROM pool_bindings WHERE pool=?", [pool])
+            for w in sorted(new):
+                self.db.execute("INSERT INTO pool_bindings (pool, workspace_id) VALUES (?, ?)", [pool, w])
+            return sorted(new)
+
+    def pools_for_workspace(self, workspace_id: int) -> List[str]:
+        """Pools a workspace's experiments may use: unbound pools + the ones bound to it."""
+        return [p for p in self.sched.pools if not self.pool_bindings(p) or int(workspace_id) in self.pool_bindings(p)]
 
     def _drop_allocation(self, a: Allocation) -> None:
         self.sched.remove_request(a.id)
@@ -715,14 +765,18 @@ class Master:
 
     # ================================================================ agents
     def register_agent(self, agent_id: str, slots: int, host: str = "127.0.0.1", devices: Optional[List[Any]] = None,
-                       gpu: bool = False, label: str = "") -> Dict[str, Any]:
+                       gpu: bool = False, label: str = "", resource_pool: Optional[str] = None) -> Dict[str, Any]:
         with self.lock:
             existing = self.agents.get(agent_id)
+            pool = resource_pool or (existing or {}).get("resource_pool") or self.sched.default_compute
+            if pool not in self.sched.pools:
+                raise KeyError(f"resource pool {pool!r} does not exist (pools: {sorted(self.sched.pools)})")
             self.agents[agent_id] = {"id": agent_id, "slots": slots, "host": host, "devices": devices or list(range(slots)),
                                      "gpu": gpu, "label": label, "queue": existing["queue"] if existing else [],
-                                     "last_seen": time.time(), "enabled": True}
+                                     "last_seen": time.time(), "enabled": existing["enabled"] if existing else True,
+                                     "resource_pool": pool}
             if existing is None:
-                self.sched.add_agent(agent_id, slots)
+                self.sched.add_agent(agent_id, slots, pool)
             self.cv.notify_all()
             return {"cluster_id": self.cluster_id}
 

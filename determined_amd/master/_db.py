@@ -44,6 +44,7 @@ CREATE TABLE IF NOT EXISTS tasks (
 CREATE TABLE IF NOT EXISTS webhooks (
   id INTEGER PRIMARY KEY AUTOINCREMENT, url TEXT, triggers TEXT, webhook_type TEXT DEFAULT 'DEFAULT');
 CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
+CREATE TABLE IF NOT EXISTS pool_bindings (pool TEXT, workspace_id INTEGER, PRIMARY KEY (pool, workspace_id));
 """
 
 MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT"),
