@@ -59,8 +59,10 @@ class _Task:
 class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, slots: Optional[int] = None,
                  gpus: Optional[List[int]] = None, work_root: Optional[str] = None, host: Optional[str] = None,
-                 token: Optional[str] = None, label: str = "", backend: Any = None) -> None:
+                 token: Optional[str] = None, label: str = "", backend: Any = None,
+                 resource_pool: Optional[str] = None) -> None:
         self.session = Session(master_url, token=token)
+        self.resource_pool = resource_pool  # None: the master's default compute pool
         self.backend = backend or ProcessBackend()
         self.agent_id = agent_id or socket.gethostname()
         self.gpus = detect_gpus() if gpus is None else gpus
@@ -76,7 +78,8 @@ class Agent:
     def register(self) -> None:
         self.session.post("/api/v1/agents/register", {"agent_id": self.agent_id, "slots": len(self.devices),
                                                       "host": self.host, "devices": self.devices,
-                                                      "gpu": self.use_gpu, "label": self.label})
+                                                      "gpu": self.use_gpu, "label": self.label,
+                                                      "resource_pool": self.resource_pool})
         logger.info(f"agent {self.agent_id} registered {len(self.devices)} {'GPU' if self.use_gpu else 'CPU'} slots")
 
     def run(self) -> None:

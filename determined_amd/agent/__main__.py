@@ -19,6 +19,7 @@ def main(argv=None) -> int:
     p.add_argument("--work-root", default=None)
     p.add_argument("--host", default=None, help="address other agents/ranks use to reach this node")
     p.add_argument("--label", default="")
+    p.add_argument("--resource-pool", default=None, help="pool to join (default: the master's default compute pool)")
     p.add_argument("--backend", default="process", choices=["process", "slurm", "pbs", "kubernetes"],
                    help="where tasks run: local process groups, Slurm/PBS batch jobs, or Kubernetes pods")
     p.add_argument("--gpu-slots", type=int, default=None,
@@ -47,7 +48,8 @@ def main(argv=None) -> int:
     if backend is not None and a.slots is None and gpus is None:
         p.error(f"--backend {a.backend} fronts a whole partition: give its GPU capacity with --gpu-slots N")
     agent = Agent(a.master_url, a.agent_id, a.slots, gpus, a.work_root, a.host,
-                  token=os.environ.get("DET_MASTER_TOKEN"), label=a.label, backend=backend)
+                  token=os.environ.get("DET_MASTER_TOKEN"), label=a.label, backend=backend,
+                  resource_pool=a.resource_pool)
     try:
         agent.run()
     except KeyboardInterrupt:

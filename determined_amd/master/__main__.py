@@ -12,7 +12,8 @@ from determined_amd.master import Master, MasterServer
 
 def main(argv=None) -> int:
     p = argparse.ArgumentParser("determined_amd.master")
-    p.add_argument("--config-file", default=None, help="master.yaml (keys: host, port, db, scheduler, fit, ...)")
+    p.add_argument("--config-file", default=None,
+                   help="master.yaml (keys: host, port, db, scheduler, fit, auth, resource_pools, resource_manager)")
     p.add_argument("--host", default=None)
     p.add_argument("--port", type=int, default=None)
     p.add_argument("--db", default=None, help="sqlite path (default ~/.local/share/determined_amd/master.db)")
@@ -32,11 +33,14 @@ def main(argv=None) -> int:
     db = a.db or cfg.get("db") or os.path.expanduser("~/.local/share/determined_amd/master.db")
     if db != ":memory:":
         os.makedirs(os.path.dirname(db), exist_ok=True)
+    rm = cfg.get("resource_manager") or {}  # reference master.yaml: resource_manager + resource_pools
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     m = Master(db_path=db, policy=a.scheduler or cfg.get("scheduler", "priority"), fit=a.fit or cfg.get("fit", "best"),
                preemption=not a.no_preemption and cfg.get("preemption", True),
                master_url=cfg.get("advertised_url", f"http://{host}:{port}"), auth_token=a.auth_token,
-               auth=a.auth or cfg.get("auth", "none"))
+               auth=a.auth or cfg.get("auth", "none"), resource_pools=cfg.get("resource_pools"),
+               default_compute_pool=rm.get("default_compute_resource_pool"),
+               default_aux_pool=rm.get("default_aux_resource_pool"))
     srv = MasterServer(m, host, port)
     logging.getLogger("determined_amd.master").info(f"master listening on http://{host}:{srv.port}")
     try:

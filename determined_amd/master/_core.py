@@ -770,7 +770,7 @@ class Master:
             existing = self.agents.get(agent_id)
             pool = resource_pool or (existing or {}).get("resource_pool") or self.sched.default_compute
             if pool not in self.sched.pools:
-                raise KeyError(f"resource pool {pool!r} does not exist (pools: {sorted(self.sched.pools)})")
+                raise ValueError(f"resource pool {pool!r} does not exist (pools: {sorted(self.sched.pools)})")
             self.agents[agent_id] = {"id": agent_id, "slots": slots, "host": host, "devices": devices or list(range(slots)),
                                      "gpu": gpu, "label": label, "queue": existing["queue"] if existing else [],
                                      "last_seen": time.time(), "enabled": existing["enabled"] if existing else True,

@@ -69,7 +69,8 @@ def add_ntsc_routes(route: Callable[[str, str], Callable], m: Any) -> None:
                     from determined_amd.master._server import HTTPError
 
                     raise HTTPError(400, str(e))
-                tid = m.create_command(cmd, int(b.get("slots", 0)), env, kind, b.get("workdir_b64"))
+                tid = m.create_command(cmd, int(b.get("slots", 0)), env, kind, b.get("workdir_b64"),
+                                       b.get("resource_pool"), b.get("priority"))
                 return {"task_id": tid, "type": kind}
             return create
 

@@ -363,7 +363,7 @@ def build_routes(m: Master) -> List[Route]:
     @route("POST", "/api/v1/commands")
     def create_cmd(q, b):
         tid = m.create_command(b["command"], int(b.get("slots", 0)), b.get("env"), b.get("type", "COMMAND"),
-                               b.get("workdir_b64"))
+                               b.get("workdir_b64"), b.get("resource_pool"), b.get("priority"))
         return {"task_id": tid}
 
     @route("POST", r"/api/v1/tasks/([^/]+)/proxy")
@@ -396,7 +396,7 @@ def build_routes(m: Master) -> List[Route]:
     @route("POST", "/api/v1/agents/register")
     def reg_agent(q, b):
         return m.register_agent(b["agent_id"], int(b["slots"]), b.get("host", "127.0.0.1"), b.get("devices"),
-                                bool(b.get("gpu")), b.get("label", ""))
+                                bool(b.get("gpu")), b.get("label", ""), b.get("resource_pool"))
 
     @route("GET", r"/api/v1/agents/([^/]+)/work")
     def agent_work(q, b, agent_id):
@@ -418,6 +418,7 @@ def build_routes(m: Master) -> List[Route]:
             owners = sa.get(aid, {}).get("slot_owner", [])
             out.append({"id": aid, "host": ag["host"], "slots": ag["slots"], "devices": ag["devices"],
                         "gpu": ag["gpu"], "enabled": ag["enabled"], "label": ag["label"],
+                        "resource_pool": ag.get("resource_pool", m.sched.default_compute),
                         "slot_owner": owners, "used_slots": sum(1 for o in owners if o)})
         return {"agents": out}
 
@@ -430,14 +431,51 @@ def build_routes(m: Master) -> List[Route]:
                 m.sched.set_agent_enabled(agent_id, what == "enable")
         return {}
 
+    def _ws_names(ids):
+        rows = {int(r["id"]): r["name"] for r in m.db.all("SELECT id, name FROM workspaces")}
+        return [rows.get(i, str(i)) for i in ids]
+
     @route("GET", "/api/v1/resource-pools")
     def pools(q, b):
-        return {"resource_pools": [{"name": "default", "scheduler_type": m.policy, "slots_available": m.sched.total_slots,
-                                    "slots_used": m.sched.used_slots, "num_agents": len(m.agents)}]}
+        with m.lock:
+            rows = m.sched.summary()
+            for r in rows:
+                r["bound_workspaces"] = _ws_names(m.pool_bindings(r["name"]))
+        return {"resource_pools": rows}
+
+    def _ws_ids(b):
+        ids = [int(w) for w in b.get("workspace_ids") or []]
+        for name in b.get("workspace_names") or []:
+            ids.append(int(m.iam.workspace(name)["id"]))
+        return ids
+
+    @route("GET", r"/api/v1/resource-pools/([^/]+)/workspace-bindings")
+    def pool_bindings(q, b, pool):
+        if pool not in m.sched.pools:
+            raise HTTPError(404, f"resource pool {pool} not found")
+        ids = m.pool_bindings(pool)
+        return {"workspace_ids": ids, "workspaces": _ws_names(ids)}
+
+    def _bind(mode):
+        def fn(q, b, pool):
+            m.iam.require("admin_cluster")
+            ids = m.set_pool_bindings(pool, _ws_ids(b), mode)
+            return {"workspace_ids": ids, "workspaces": _ws_names(ids)}
+        return fn
+
+    route("POST", r"/api/v1/resource-pools/([^/]+)/workspace-bindings")(_bind("add"))
+    route("PUT", r"/api/v1/resource-pools/([^/]+)/workspace-bindings")(_bind("replace"))
+    route("DELETE", r"/api/v1/resource-pools/([^/]+)/workspace-bindings")(_bind("remove"))
+
+    @route("GET", r"/api/v1/workspaces/([^/]+)/available-resource-pools")
+    def ws_pools(q, b, ref):
+        w = m.iam.workspace(ref)
+        m.iam.require("view", w["id"])
+        return {"resource_pools": m.pools_for_workspace(int(w["id"]))}
 
     @route("GET", "/api/v1/job-queues")
     def jobs(q, b):
-        return {"jobs": list(m.sched.requests().values())}
+        return {"jobs": list(m.sched.requests(q.get("resource_pool") or None).values())}
 
     # ---------------------------------------------------------------- model registry
     @route("POST", "/api/v1/models")
@@ -616,6 +654,8 @@ class _Handler(BaseHTTPRequestHandler):
                 data = json.dumps(out, default=str).encode()
         except (HTTPError, AuthError) as e:
             status, data = e.status, json.dumps({"error": e.message}).encode()
+        except ValueError as e:  # invalid request content (e.g. an unknown resource pool)
+            status, data = 400, json.dumps({"error": str(e)}).encode()
         except KeyError as e:
             status, data = 404, json.dumps({"error": str(e)}).encode()
         except Exception as e:  # noqa: BLE001

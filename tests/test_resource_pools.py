@@ -1,0 +1,90 @@
+"""Resource pools (reference: master config ``resource_pools``, ``rm/agentrm/resource_pool.go``,
+workspace bindings ``api_resourcepool.go``): per-pool schedulers, agents / trials / commands
+landing in the right pool, defaults, job queues per pool, workspace bindings."""
+
+import pytest
+
+from determined_amd.common.api import APIException, Session
+
+POOLS = [{"pool_name": "train", "scheduler": {"type": "fair_share"}},
+         {"pool_name": "aux", "description": "notebooks", "scheduler": {"type": "round_robin"}}]
+CFG = {"name": "p", "entrypoint": "model_def:T", "hyperparameters": {},
+       "searcher": {"name": "single", "metric": "loss", "max_length": {"batches": 1}}}
+
+
+@pytest.fixture()
+def pooled():
+    from determined_amd.master import start_master
+
+    srv = start_master(resource_pools=POOLS, default_compute_pool="train", default_aux_pool="aux")
+    yield srv, Session(f"http://127.0.0.1:{srv.port}")
+    srv.stop()
+    srv.master.close()
+
+
+def _assigned(m, task_id):
+    with m.lock:
+        m._schedule()
+        a = next(a for a in m.allocations.values() if a.task_id == task_id)
+        return [ag for ag, _ in a.assignment]
+
+
+def test_agents_and_tasks_land_in_their_pools(pooled):
+    srv, s = pooled
+    m = srv.master
+    s.post("/api/v1/agents/register", {"agent_id": "gpu-node", "slots": 8, "resource_pool": "train"})
+    s.post("/api/v1/agents/register", {"agent_id": "cpu-node", "slots": 2, "resource_pool": "aux"})
+    with pytest.raises(APIException) as e:
+        s.post("/api/v1/agents/register", {"agent_id": "x", "slots": 1, "resource_pool": "nope"})
+    assert e.value.status == 400
+    pools = {p["name"]: p for p in s.get("/api/v1/resource-pools")["resource_pools"]}
+    assert pools["train"]["slots_available"] == 8 and pools["train"]["scheduler_type"] == "fair_share"
+    assert pools["aux"]["slots_available"] == 2 and pools["aux"]["default_aux_pool"]
+    assert {a["id"]: a["resource_pool"] for a in s.get("/api/v1/agents")["agents"]} == {"gpu-node": "train",
+                                                                                      "cpu-node": "aux"}
+    # slots > 0 -> default compute pool; 0 slots -> default aux pool; explicit pool wins
+    t1 = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 4})["task_id"]
+    t0 = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 0})["task_id"]
+    t2 = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 1, "resource_pool": "aux"})["task_id"]
+    assert _assigned(m, t1) == ["gpu-node"]
+    assert _assigned(m, t2) == ["cpu-node"]
+    jobs = s.get("/api/v1/job-queues", params={"resource_pool": "aux"})["jobs"]
+    assert {j["job_id"] for j in jobs} == {t0, t2} and all(j["resource_pool"] == "aux" for j in jobs)
+    # a request larger than its pool never spills into another pool
+    big = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 3, "resource_pool": "aux"})["task_id"]
+    assert _assigned(m, big) == []
+
+
+def test_experiment_pool_validation_and_workspace_bindings(pooled):
+    srv, s = pooled
+    with pytest.raises(APIException) as e:
+        s.post("/api/v1/experiments", {"config": dict(CFG, resources={"resource_pool": "nope"}), "activate": False})
+    assert e.value.status == 400
+    eid = s.post("/api/v1/experiments", {"config": CFG, "activate": False})["experiment"]["id"]
+    assert srv.master.experiments[eid].config["resources"]["resource_pool"] == "train"
+    ws = s.post("/api/v1/workspaces", {"name": "vision"})["workspace"]
+    s.post(f"/api/v1/workspaces/{ws['id']}/projects", {"name": "detection"})
+    got = s.request("PUT", "/api/v1/resource-pools/train/workspace-bindings", body={"workspace_names": ["vision"]})
+    assert got["workspaces"] == ["vision"]
+    assert s.get("/api/v1/resource-pools/train/workspace-bindings")["workspaces"] == ["vision"]
+    with pytest.raises(APIException) as e:  # the Uncategorized workspace may no longer use "train"
+        s.post("/api/v1/experiments", {"config": CFG, "activate": False})
+    assert e.value.status == 400
+    s.post("/api/v1/experiments", {"config": dict(CFG, workspace="vision", project="detection"), "activate": False})
+    assert s.get("/api/v1/workspaces/Uncategorized/available-resource-pools")["resource_pools"] == ["aux"]
+    assert sorted(s.get("/api/v1/workspaces/vision/available-resource-pools")["resource_pools"]) == ["aux", "train"]
+    s.request("DELETE", "/api/v1/resource-pools/train/workspace-bindings", body={"workspace_names": ["vision"]})
+    assert s.get("/api/v1/resource-pools/train/workspace-bindings")["workspaces"] == []
+
+
+def test_single_default_pool_without_config():
+    from determined_amd.master import start_master
+
+    srv = start_master()
+    try:
+        s = Session(f"http://127.0.0.1:{srv.port}")
+        (p,) = s.get("/api/v1/resource-pools")["resource_pools"]
+        assert p["name"] == "default" and p["default_compute_pool"] and p["default_aux_pool"]
+    finally:
+        srv.stop()
+        srv.master.close()
