@@ -113,9 +113,23 @@ class ProcessBackend:
     def launch(self, argv: List[str], workdir: pathlib.Path, env: Dict[str, str], cmd: Dict[str, Any]) -> TaskHandle:
         full = dict(os.environ)
         full.update(env)
+        uid, gid = run_as(env)
+        if uid is not None:  # the owner's linked agent user (det user link-with-agent-user)
+            os.chown(workdir, uid, gid if gid is not None else -1)
         proc = subprocess.Popen(argv, cwd=workdir, env=full, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                start_new_session=True, text=True, bufsize=1)
+                                start_new_session=True, text=True, bufsize=1, user=uid,
+                                group=gid if uid is not None else None)
         return _ProcessHandle(proc)
+
+
+def run_as(env: Dict[str, str]):
+    """(uid, gid) a task should run as: the task owner's linked agent user when the master sent
+    one (DET_AGENT_UID / DET_AGENT_GID) and this agent runs as root (it can switch users); else
+    (None, None) -- the task runs as the agent's own user."""
+    if "DET_AGENT_UID" not in env or not hasattr(os, "geteuid") or os.geteuid() != 0:
+        return None, None
+    gid = env.get("DET_AGENT_GID")
+    return int(env["DET_AGENT_UID"]), (int(gid) if gid not in (None, "") else None)
 
 
 # ------------------------------------------------------------------------------------ batch jobs

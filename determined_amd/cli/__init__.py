@@ -310,7 +310,9 @@ def job_list(a):
 
 def cmd_run(a):
     s = _session(a)
-    r = s.post("/api/v1/commands", {"command": " ".join(a.cmd), "slots": a.slots})
+    r = s.post("/api/v1/commands", {"command": " ".join(a.cmd), "slots": a.slots,
+                                    "resource_pool": getattr(a, "resource_pool", None),
+                                    "priority": getattr(a, "priority", None)})
     print(f"Launched command {r['task_id']}")
     if not a.detach:
         _follow_logs(s, r["task_id"], lambda: s.get(f"/api/v1/tasks/{r['task_id']}")["task"]["state"] in
@@ -526,7 +528,7 @@ def build_parser() -> argparse.ArgumentParser:
     ts.set_defaults(fn=template_set)
     tp.add_parser("list").set_defaults(fn=template_list)
 
-    wh = sub.add_parser("webhook", aliases=["w"]).add_subparsers(dest="verb", required=True)
+    wh = sub.add_parser("webhook").add_subparsers(dest="verb", required=True)
     wc = wh.add_parser("create")
     wc.add_argument("url")
     wc.add_argument("--trigger", action="append")
@@ -537,6 +539,10 @@ def build_parser() -> argparse.ArgumentParser:
 
     _iam.register(sub, _session, _print)
     _iam.register_experiment_move(e, _session)
+
+    from determined_amd.cli import _more
+
+    _more.register(sub, _session, _print, _follow_logs)
 
     dp = sub.add_parser("deploy").add_subparsers(dest="where", required=True)
     loc = dp.add_parser("local").add_subparsers(dest="verb", required=True)

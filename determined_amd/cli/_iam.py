@@ -188,6 +188,12 @@ def register(sub: Any, session: Any, show: Any) -> None:
 
     def assign(remove):
         def fn(a):
+            if bool(a.username) == bool(a.group_name):
+                raise SystemExit("give exactly one of --username-to-assign / --group-name-to-assign")
+            if a.group_name:
+                session(a).post("/api/v1/rbac/unassign-group" if remove else "/api/v1/rbac/assign-group",
+                                {"group": a.group_name, "role": a.role, "workspace": a.workspace_name})
+                return
             session(a).post("/api/v1/rbac/unassign" if remove else "/api/v1/rbac/assign",
                             {"user": a.username, "role": a.role, "workspace": a.workspace_name})
         return fn
@@ -200,7 +206,8 @@ def register(sub: Any, session: Any, show: Any) -> None:
     for verb, remove in (("assign-role", False), ("unassign-role", True)):
         p = rb.add_parser(verb)
         p.add_argument("role")
-        p.add_argument("--username-to-assign", "--username", dest="username", required=True)
+        p.add_argument("--username-to-assign", "--username", dest="username", default=None)
+        p.add_argument("--group-name-to-assign", "--group-name", dest="group_name", default=None)
         p.add_argument("--workspace-name", default=None)
         p.set_defaults(fn=assign(remove))
 

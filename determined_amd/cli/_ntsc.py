@@ -46,6 +46,11 @@ def shell_command(task: Dict[str, Any]) -> Dict[str, Any]:
     return {"argv": ["ssh", "-t", px["host"], remote], "env": {}, "cwd": None}
 
 
+def _pool_args(a: Any) -> Dict[str, Any]:
+    """--resource-pool / --priority (added by cli/_more.py to every task-creating verb)."""
+    return {k: getattr(a, k, None) for k in ("resource_pool", "priority")}
+
+
 def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
     cols = ["id", "type", "state", "exit_code"]
 
@@ -78,7 +83,8 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
     # ---------------------------------------------------------------- tensorboard
     def tb_start(a):
         s = session(a)
-        r = s.post("/api/v1/tensorboards", {"experiment_ids": a.experiment_ids, "trial_ids": a.trial_id or []})
+        r = s.post("/api/v1/tensorboards", {"experiment_ids": a.experiment_ids, "trial_ids": a.trial_id or [],
+                                            **_pool_args(a)})
         t = _wait_proxy(s, r["task_id"])
         print(f"Launched tensorboard {r['task_id']}: http://{t['proxy']['host']}:{t['proxy']['port']}/")
 
@@ -96,7 +102,7 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
     # ---------------------------------------------------------------- notebook
     def nb_start(a):
         s = session(a)
-        r = s.post("/api/v1/notebooks", {"slots": a.slots})
+        r = s.post("/api/v1/notebooks", {"slots": a.slots, **_pool_args(a)})
         t = _wait_proxy(s, r["task_id"])
         print(f"Launched notebook {r['task_id']}: http://{t['proxy']['host']}:{t['proxy']['port']}/lab")
 
@@ -105,7 +111,7 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
     # ---------------------------------------------------------------- shell
     def sh_start(a):
         s = session(a)
-        r = s.post("/api/v1/shells", {"slots": a.slots, "idle_timeout": a.idle_timeout})
+        r = s.post("/api/v1/shells", {"slots": a.slots, "idle_timeout": a.idle_timeout, **_pool_args(a)})
         _wait_proxy(s, r["task_id"])
         print(f"Launched shell {r['task_id']}")
         if not a.detach:

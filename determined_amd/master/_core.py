@@ -566,6 +566,20 @@ class Master:
             self.cv.notify_all()
             return task_id
 
+    def set_task_priority(self, task_id: str, priority: Optional[int] = None, weight: Optional[float] = None) -> None:
+        """``det notebook|shell|tensorboard|command set priority`` / ``det job update``."""
+        with self.lock:
+            row = self.db.one("SELECT config FROM tasks WHERE id=?", [task_id])
+            cfg = dict((row or {}).get("config") or {})
+            if priority is not None:
+                cfg["priority"] = int(priority)
+                self.sched.set_priority(task_id, int(priority))
+            if weight is not None:
+                cfg["weight"] = float(weight)
+                self.sched.set_weight(task_id, float(weight))
+            self.db.update("tasks", "id", task_id, config=cfg)
+            self.cv.notify_all()
+
     # ================================================================ resource pools
     def check_pool(self, name: Optional[str], slots: int, workspace: Optional[str]) -> str:
         """The pool a request lands in (named, or the compute / aux default by slots); a pool bound
@@ -583,6 +597,17 @@ class Master:
                 if w is None or int(w["id"]) not in bound:
                     raise ValueError(f"resource pool {pool!r} is bound to other workspaces than {workspace!r}")
         return pool
+
+    def allocation_usage(self, after: float, before: float) -> List[Dict[str, Any]]:
+        """Allocations that held slots in [after, before), with the overlap in seconds."""
+        now = time.time()
+        rows = self.db.all("SELECT * FROM allocation_history WHERE start_time < ? AND (end_time IS NULL OR end_time > ?) "
+                           "ORDER BY start_time", [before, after])
+        for r in rows:
+            end = r["end_time"] if r["end_time"] is not None else now
+            r["seconds"] = max(0.0, min(end, before) - max(r["start_time"], after))
+            r["slot_seconds"] = r["seconds"] * int(r["slots"] or 0)
+        return rows
 
     def pool_bindings(self, pool: str) -> List[int]:
         return [int(r["workspace_id"]) for r in self.db.all("SELECT workspace_id FROM pool_bindings WHERE pool=? "
@@ -706,6 +731,7 @@ class Master:
             reqs = reqs or self.sched.requests()
             a.assignment = [(ag, list(sl)) for ag, sl in reqs[aid]["assignment"]]
             a.state = "ASSIGNED"
+            self._record_allocation_start(a, reqs[aid].get("resource_pool"))
             self._dispatch(a)
         for aid in d["preempt"]:
             a = self.allocations.get(aid)
@@ -753,6 +779,7 @@ class Master:
                 for kv in _env_list(cfg.get("environment", {}).get("environment_variables")):
                     k, _, v = kv.partition("=")
                     env[k] = v
+                env.update(self._agent_user_env(a.exp_id))
                 cmd.update(entrypoint=cfg.get("entrypoint"), slots_per_trial=a.slots,
                            model_def_url=f"/api/v1/experiments/{exp.id}/model_def")
                 self._persist_trial(tr)
@@ -820,9 +847,33 @@ class Master:
                     self._finish_allocation(a)
             self.cv.notify_all()
 
+    def _agent_user_env(self, exp_id: Optional[int]) -> Dict[str, str]:
+        """The experiment owner's linked agent user/group (``det user link-with-agent-user``)."""
+        row = self.db.one("SELECT u.agent_uid, u.agent_gid, u.agent_user, u.agent_group FROM experiments e "
+                          "JOIN users u ON u.username = e.owner WHERE e.id=?", [exp_id]) if exp_id is not None else None
+        out: Dict[str, str] = {}
+        for col, key in (("agent_uid", "DET_AGENT_UID"), ("agent_gid", "DET_AGENT_GID"),
+                         ("agent_user", "DET_AGENT_USER"), ("agent_group", "DET_AGENT_GROUP")):
+            if row is not None and row.get(col) is not None:
+                out[key] = str(row[col])
+        return out
+
+    def _record_allocation_start(self, a: Allocation, pool: Optional[str]) -> None:
+        """Slot usage history (``det resources raw|aggregated``; reference
+        ``master/internal/db/postgres_resourcemanagers`` allocation accounting)."""
+        owner = None
+        if a.exp_id is not None and a.exp_id in self.experiments:
+            row = self.db.one("SELECT owner FROM experiments WHERE id=?", [a.exp_id])
+            owner = row["owner"] if row else None
+        self.db.execute("INSERT OR REPLACE INTO allocation_history (alloc_id, task_id, kind, experiment_id, owner, "
+                        "resource_pool, slots, start_time, end_time) VALUES (?, ?, ?, ?, ?, ?, ?, ?, NULL)",
+                        [a.id, a.task_id, a.kind, a.exp_id, owner, pool, a.slots, time.time()])
+
     def _finish_allocation(self, a: Allocation) -> None:
         if a.state == "TERMINATED":
             return
+        self.db.execute("UPDATE allocation_history SET end_time=? WHERE alloc_id=? AND end_time IS NULL",
+                        [time.time(), a.id])
         self.sched.remove_request(a.id)
         a.state = "TERMINATED"
         self._on_allocation_exit(a)

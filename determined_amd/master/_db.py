@@ -44,6 +44,9 @@ CREATE TABLE IF NOT EXISTS tasks (
 CREATE TABLE IF NOT EXISTS webhooks (
   id INTEGER PRIMARY KEY AUTOINCREMENT, url TEXT, triggers TEXT, webhook_type TEXT DEFAULT 'DEFAULT');
 CREATE TABLE IF NOT EXISTS templates (name TEXT PRIMARY KEY, config TEXT);
+CREATE TABLE IF NOT EXISTS allocation_history (
+  alloc_id TEXT PRIMARY KEY, task_id TEXT, kind TEXT, experiment_id INTEGER, owner TEXT, resource_pool TEXT,
+  slots INTEGER, start_time REAL, end_time REAL);
 CREATE TABLE IF NOT EXISTS pool_bindings (pool TEXT, workspace_id INTEGER, PRIMARY KEY (pool, workspace_id));
 """
 

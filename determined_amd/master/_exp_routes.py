@@ -116,8 +116,11 @@ def add_exp_routes(route: Callable[[str, str], Callable], m: Any) -> None:
     def update_jobs(q, b):
         for u in b.get("updates", []):
             job = str(u["job_id"])
-            if not job.startswith("exp-"):
-                raise HTTPError(400, f"only experiment jobs can be updated, got {job}")
+            if not job.startswith("exp-"):  # a command / notebook / shell / tensorboard task
+                if m.db.one("SELECT id FROM tasks WHERE id=?", [job]) is None:
+                    raise HTTPError(404, f"job {job} not found")
+                m.set_task_priority(job, u.get("priority"), u.get("weight"))
+                continue
             eid = int(job.split("-", 1)[1])
             _guard_exp(m, eid, "edit")
             m.set_experiment_resources(eid, weight=u.get("weight"), priority=u.get("priority"))

@@ -39,7 +39,15 @@ CREATE TABLE IF NOT EXISTS projects (
 CREATE TABLE IF NOT EXISTS role_assignments (
   id INTEGER PRIMARY KEY AUTOINCREMENT, user_id INTEGER, role TEXT, workspace_id INTEGER,
   UNIQUE(user_id, role, workspace_id));
+CREATE TABLE IF NOT EXISTS user_groups (id INTEGER PRIMARY KEY AUTOINCREMENT, name TEXT UNIQUE, created REAL);
+CREATE TABLE IF NOT EXISTS group_members (group_id INTEGER, user_id INTEGER, PRIMARY KEY (group_id, user_id));
+CREATE TABLE IF NOT EXISTS group_role_assignments (
+  id INTEGER PRIMARY KEY AUTOINCREMENT, group_id INTEGER, role TEXT, workspace_id INTEGER,
+  UNIQUE(group_id, role, workspace_id));
 """
+# the user's identity on the agents (reference ``det user link-with-agent-user``): tasks the user
+# owns run with this uid/gid where the agent may switch users (it runs as root)
+AGENT_USER_COLS = (("agent_uid", "INTEGER"), ("agent_gid", "INTEGER"), ("agent_user", "TEXT"), ("agent_group", "TEXT"))
 
 # permission -> minimum role rank (scoped roles are checked against the object's workspace)
 ROLES = {"Viewer": 1, "Editor": 2, "WorkspaceAdmin": 3, "ClusterAdmin": 4, "WorkspaceCreator": 0}
@@ -78,8 +86,12 @@ def check_password(password: str, stored: str) -> bool:
 
 
 def _public_user(u: Dict[str, Any]) -> Dict[str, Any]:
-    return {"id": u["id"], "username": u["username"], "display_name": u.get("display_name") or "",
-            "admin": bool(u["admin"]), "active": bool(u["active"])}
+    out = {"id": u["id"], "username": u["username"], "display_name": u.get("display_name") or "",
+           "admin": bool(u["admin"]), "active": bool(u["active"])}
+    agent = {k: u.get(k) for k, _ in AGENT_USER_COLS if u.get(k) is not None}
+    if agent:
+        out["agent_user_group"] = agent
+    return out
 
 
 class IAM:
@@ -91,6 +103,10 @@ class IAM:
         self.cluster_token = cluster_token
         self._local = threading.local()
         db.conn.executescript(SCHEMA)
+        have = {r[1] for r in db.conn.execute("PRAGMA table_info(users)").fetchall()}
+        for col, typ in AGENT_USER_COLS:
+            if col not in have:
+                db.conn.execute(f"ALTER TABLE users ADD COLUMN {col} {typ}")
         self._bootstrap()
 
     # ------------------------------------------------------------------ bootstrap
@@ -157,7 +173,7 @@ class IAM:
     def _rank(self, user: Dict[str, Any], workspace_id: Optional[int]) -> int:
         if user["admin"]:
             return ROLES["ClusterAdmin"]
-        rows = self.db.all("SELECT role, workspace_id FROM role_assignments WHERE user_id=?", [user["id"]])
+        rows = self._role_rows(user)
         best = 0
         for r in rows:
             if r["workspace_id"] is None or (workspace_id is not None and r["workspace_id"] == workspace_id):
@@ -167,9 +183,14 @@ class IAM:
     def has_role(self, user: Dict[str, Any], role: str, workspace_id: Optional[int] = None) -> bool:
         if user["admin"]:
             return True
-        rows = self.db.all("SELECT role, workspace_id FROM role_assignments WHERE user_id=? AND role=?",
-                           [user["id"], role])
+        rows = [r for r in self._role_rows(user) if r["role"] == role]
         return any(r["workspace_id"] is None or r["workspace_id"] == workspace_id for r in rows)
+
+    def _role_rows(self, user: Dict[str, Any]) -> List[Dict[str, Any]]:
+        """The user's own role assignments plus those of every group it belongs to."""
+        return self.db.all("SELECT role, workspace_id FROM role_assignments WHERE user_id=? UNION ALL "
+                           "SELECT g.role, g.workspace_id FROM group_role_assignments g JOIN group_members m "
+                           "ON m.group_id = g.group_id WHERE m.user_id=?", [user["id"], user["id"]])
 
     def can(self, perm: str, workspace_id: Optional[int] = None, owner_id: Optional[int] = None,
             user: Optional[Dict[str, Any]] = None) -> bool:
@@ -236,6 +257,9 @@ class IAM:
         for k in ("admin", "active"):
             if k in body:
                 cols[k] = int(bool(body[k]))
+        for k, _ in AGENT_USER_COLS:  # link-with-agent-user (admin only, checked above)
+            if k in body:
+                cols[k] = body[k]
         if cols:
             self.db.update("users", "id", u["id"], **cols)
         return _public_user(self.get_user(str(u["id"])))
@@ -402,6 +426,90 @@ class IAM:
                                  [u["id"], role, wid])
         if exists is None:
             self.db.insert("role_assignments", user_id=u["id"], role=role, workspace_id=wid)
+
+    # ------------------------------------------------------------------ user groups
+    def group(self, ref: Any) -> Dict[str, Any]:
+        g = self.db.one("SELECT * FROM user_groups WHERE id=?", [int(ref)]) if str(ref).isdigit() else \
+            self.db.one("SELECT * FROM user_groups WHERE name=?", [ref])
+        if g is None:
+            raise AuthError(404, f"user group {ref} not found")
+        members = self.db.all("SELECT u.id, u.username FROM group_members m JOIN users u ON u.id = m.user_id "
+                              "WHERE m.group_id=? ORDER BY u.username", [g["id"]])
+        return {"id": g["id"], "name": g["name"], "members": [m["username"] for m in members],
+                "num_members": len(members)}
+
+    def list_groups(self, user_ref: Optional[str] = None) -> List[Dict[str, Any]]:
+        rows = self.db.all("SELECT id FROM user_groups ORDER BY name")
+        out = [self.group(r["id"]) for r in rows]
+        if user_ref:
+            name = self.get_user(user_ref)["username"]
+            out = [g for g in out if name in g["members"]]
+        return out
+
+    def create_group(self, name: str, members: Optional[List[str]] = None) -> Dict[str, Any]:
+        self.require("admin_cluster")
+        if not name or self.db.one("SELECT id FROM user_groups WHERE name=?", [name]) is not None:
+            raise AuthError(409, f"user group {name!r} already exists")
+        gid = self.db.insert("user_groups", name=name, created=time.time())
+        if members:
+            self.set_members(gid, members, add=True)
+        return self.group(gid)
+
+    def rename_group(self, ref: Any, name: str) -> Dict[str, Any]:
+        self.require("admin_cluster")
+        g = self.group(ref)
+        if not name or self.db.one("SELECT id FROM user_groups WHERE name=?", [name]) is not None:
+            raise AuthError(409, f"user group {name!r} already exists")
+        self.db.update("user_groups", "id", g["id"], name=name)
+        return self.group(g["id"])
+
+    def delete_group(self, ref: Any) -> None:
+        self.require("admin_cluster")
+        g = self.group(ref)
+        for t in ("group_members", "group_role_assignments"):
+            self.db.execute(f"DELETE FROM {t} WHERE group_id=?", [g["id"]])
+        self.db.execute("DELETE FROM user_groups WHERE id=?", [g["id"]])
+
+    def set_members(self, ref: Any, users: List[str], add: bool) -> Dict[str, Any]:
+        self.require("admin_cluster")
+        g = self.group(ref)
+        for u in users:
+            uid = self.get_user(u)["id"]
+            if add:
+                self.db.execute("INSERT OR IGNORE INTO group_members (group_id, user_id) VALUES (?, ?)", [g["id"], uid])
+            else:
+                self.db.execute("DELETE FROM group_members WHERE group_id=? AND user_id=?", [g["id"], uid])
+        return self.group(g["id"])
+
+    def assign_group(self, group_ref: Any, role: str, workspace_ref: Any = None, remove: bool = False) -> None:
+        if role not in ROLES:
+            raise AuthError(400, f"unknown role {role!r}; roles: {sorted(ROLES)}")
+        g = self.group(group_ref)
+        wid = None if workspace_ref in (None, "") else self.workspace(workspace_ref)["id"]
+        if wid is None or role in ("ClusterAdmin", "WorkspaceCreator"):
+            self.require("admin_cluster")
+        else:
+            self.require("admin_workspace", wid)
+        where = "group_id=? AND role=? AND " + ("workspace_id IS NULL" if wid is None else "workspace_id=?")
+        args = [g["id"], role] + ([] if wid is None else [wid])
+        if remove:
+            self.db.execute(f"DELETE FROM group_role_assignments WHERE {where}", args)
+        elif self.db.one(f"SELECT id FROM group_role_assignments WHERE {where}", args) is None:
+            self.db.insert("group_role_assignments", group_id=g["id"], role=role, workspace_id=wid)
+
+    def group_assignments(self) -> List[Dict[str, Any]]:
+        return self.db.all("SELECT r.id, g.name AS group_name, r.role, w.name AS workspace FROM group_role_assignments r "
+                           "JOIN user_groups g ON g.id = r.group_id LEFT JOIN workspaces w ON w.id = r.workspace_id "
+                           "ORDER BY r.id")
+
+    def my_permissions(self) -> Dict[str, Any]:
+        """The current user's effective permissions: cluster-wide and per workspace."""
+        u = self.current()
+        scopes: Dict[str, List[str]] = {}
+        wss = self.db.all("SELECT id, name FROM workspaces ORDER BY id")
+        for scope, wid in [("cluster", None)] + [(w["name"], w["id"]) for w in wss]:
+            scopes[scope] = [p for p in PERMS if self.can(p, wid, user=u)]
+        return {"username": u["username"], "mode": self.mode, "permissions": scopes}
 
     def assignments(self, user_ref: Optional[str] = None) -> List[Dict[str, Any]]:
         sql = ("SELECT r.id, u.username, r.role, w.name AS workspace FROM role_assignments r "

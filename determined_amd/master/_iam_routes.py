@@ -128,7 +128,54 @@ def add_iam_routes(route: Callable[[str, str], Callable], m: Any) -> None:
         m.db.update("experiments", "id", int(eid), project=p["name"], workspace=w["name"])
         return {}
 
+    # ---------------------------------------------------------------- user groups
+    @route("GET", "/api/v1/groups")
+    def list_groups(q, b):
+        return {"groups": iam.list_groups(q.get("user"))}
+
+    @route("POST", "/api/v1/groups")
+    def create_group(q, b):
+        return {"group": iam.create_group(b["name"], b.get("add_users"))}
+
+    @route("GET", r"/api/v1/groups/([^/]+)")
+    def get_group(q, b, ref):
+        return {"group": iam.group(ref)}
+
+    @route("PATCH", r"/api/v1/groups/([^/]+)")
+    def patch_group(q, b, ref):
+        g = iam.group(ref)
+        if b.get("name"):
+            g = iam.rename_group(ref, b["name"])
+        if b.get("add_users"):
+            g = iam.set_members(g["id"], b["add_users"], add=True)
+        if b.get("remove_users"):
+            g = iam.set_members(g["id"], b["remove_users"], add=False)
+        return {"group": g}
+
+    @route("DELETE", r"/api/v1/groups/([^/]+)")
+    def delete_group(q, b, ref):
+        iam.delete_group(ref)
+        return {}
+
     # ---------------------------------------------------------------- RBAC
+    @route("GET", "/api/v1/rbac/my-permissions")
+    def my_perms(q, b):
+        return iam.my_permissions()
+
+    @route("GET", "/api/v1/rbac/group-assignments")
+    def group_assignments(q, b):
+        return {"assignments": iam.group_assignments()}
+
+    @route("POST", "/api/v1/rbac/assign-group")
+    def assign_group(q, b):
+        iam.assign_group(b["group"], b["role"], b.get("workspace"))
+        return {}
+
+    @route("POST", "/api/v1/rbac/unassign-group")
+    def unassign_group(q, b):
+        iam.assign_group(b["group"], b["role"], b.get("workspace"), remove=True)
+        return {}
+
     @route("GET", "/api/v1/rbac/roles")
     def roles(q, b):
         return {"roles": iam.list_roles()}

@@ -88,9 +88,36 @@ def add_ntsc_routes(route: Callable[[str, str], Callable], m: Any) -> None:
     @route("GET", "/api/v1/master/config")
     def master_config(q, b):
         m.iam.require("view")
+        import logging as _logging
+
         return {"config": {"scheduler": {"type": m.policy, "fitting_policy": getattr(m, "fit", None)},
                            "auth": m.iam.mode, "master_url": m.master_url, "cluster_id": m.cluster_id,
-                           "db": m.db.path, "log_retention_days": None}}
+                           "db": m.db.path, "log_retention_days": None,
+                           "resource_pools": m.sched.summary(),
+                           "resource_manager": {"default_compute_resource_pool": m.sched.default_compute,
+                                                "default_aux_resource_pool": m.sched.default_aux},
+                           "log": {"level": _logging.getLevelName(
+                               _logging.getLogger("determined_amd").getEffectiveLevel()).lower()}}}
+
+    @route("PATCH", "/api/v1/master/config")
+    def master_config_set(q, b):
+        """Runtime-mutable master settings (reference ``det master config set --log.level``)."""
+        import logging as _logging
+
+        m.iam.require("admin_cluster")
+        level = (b.get("log") or {}).get("level")
+        if level is not None:
+            lv = _logging.getLevelName(str(level).upper())
+            if not isinstance(lv, int):
+                raise ValueError(f"unknown log level {level!r}")
+            _logging.getLogger("determined_amd").setLevel(lv)
+        return master_config(q, b)
+
+    @route("POST", "/api/v1/tasks/cleanup-logs")
+    def cleanup_logs(q, b):
+        """Apply the log retention policies now (reference ``det task cleanup-logs``)."""
+        m.iam.require("admin_cluster")
+        return {"removed": m.cleanup_logs()}
 
     @route("GET", "/api/v1/master/logs")
     def master_logs(q, b):

@@ -29,6 +29,18 @@ logger = logging.getLogger("determined_amd.master")
 Route = Tuple[str, "re.Pattern[str]", Callable[..., Any]]
 
 
+def _ts(v: Any, default: float) -> float:
+    """A query timestamp: epoch seconds or ISO-8601 (``2024-01-31T12:00:00Z``)."""
+    if v in (None, ""):
+        return default
+    try:
+        return float(v)
+    except ValueError:
+        import datetime
+
+        return datetime.datetime.fromisoformat(str(v).replace("Z", "+00:00")).timestamp()
+
+
 class HTTPError(Exception):
     def __init__(self, status: int, message: str) -> None:
         super().__init__(message)
@@ -472,6 +484,42 @@ def build_routes(m: Master) -> List[Route]:
         w = m.iam.workspace(ref)
         m.iam.require("view", w["id"])
         return {"resource_pools": m.pools_for_workspace(int(w["id"]))}
+
+    @route("GET", "/api/v1/resources/allocation/raw")
+    def alloc_raw(q, b):
+        return {"allocations": m.allocation_usage(_ts(q.get("timestamp_after"), 0.0),
+                                                  _ts(q.get("timestamp_before"), time.time() + 1))}
+
+    @route("GET", "/api/v1/resources/allocation/aggregated")
+    def alloc_agg(q, b):
+        """Slot-hours per day (or month) in [start_date, end_date], by experiment owner, experiment,
+        resource pool and task kind (reference ``api_resources.go`` ResourceAllocationAggregated)."""
+        import datetime
+
+        period = (q.get("period") or "DAILY").upper()
+        d0 = datetime.date.fromisoformat(q["start_date"])
+        d1 = datetime.date.fromisoformat(q["end_date"])
+        out = []
+        day = d0
+        while day <= d1:
+            if period == "MONTHLY":
+                nxt = (day.replace(day=1) + datetime.timedelta(days=32)).replace(day=1)
+            else:
+                nxt = day + datetime.timedelta(days=1)
+            t0 = datetime.datetime.combine(day, datetime.time()).timestamp()
+            t1 = datetime.datetime.combine(nxt, datetime.time()).timestamp()
+            agg = {"period_start": day.isoformat(), "period": period, "seconds": 0.0, "by_username": {},
+                   "by_experiment_id": {}, "by_resource_pool": {}, "by_kind": {}}
+            for r in m.allocation_usage(t0, t1):
+                ss = r["slot_seconds"]
+                agg["seconds"] += ss
+                for key, val in (("by_username", r["owner"]), ("by_experiment_id", r["experiment_id"]),
+                                 ("by_resource_pool", r["resource_pool"]), ("by_kind", r["kind"])):
+                    if val is not None:
+                        agg[key][str(val)] = agg[key].get(str(val), 0.0) + ss
+            out.append(agg)
+            day = nxt
+        return {"resource_entries": out}
 
     @route("GET", "/api/v1/job-queues")
     def jobs(q, b):
