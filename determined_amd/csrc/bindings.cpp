@@ -79,7 +79,7 @@ extern "C" int damd_wgrad_launch(const void*, const void*, float*, void*, int, i
 extern "C" int damd_conv_fwd_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int,
                                     int, int, int, hipStream_t, int, const void*, const void*, const uint8_t*,
                                     const float*, const float*, const float*, int, const void*, const float*,
-                                    const float*, const float*, void*, uint8_t*, float*, int*, int);
+                                    const float*, const float*, void*, uint8_t*, float*, int*, int, int ophase = 0);
 extern "C" int damd_conv_pro_supported(int, int, int, int, int, int, int);
 extern "C" void damd_occupy_launch(int, double, int*, hipStream_t);
 extern "C" int damd_conv_pro_supported_w(int, int, int, int, int, int, int, int);
@@ -837,6 +837,30 @@ bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg, int64
                              static_cast<int>(x.size(3)), static_cast<int>(cfg));
 }
 
+// One phase (a, b) of the input gradient of a stride-2, pad-1 3x3 conv (even input size 2*OH x 2*OW):
+// dX[n, 2i+a, 2j+b] = sum over the phase's taps of dY[n, i+dh, j+dw] . W[k, c, r, s] -- a stride-1,
+// pad-0 conv of dY with the (1|2)x(1|2) sub-kernel wsub ([C][Rp][Sp][K] channels-last, taps ordered by
+// dh, dw = 0, +1), written straight into its pixels of dX (conv_igemm.hip Geo::ost).
+void conv_dgrad_phase(const at::Tensor& dy, const at::Tensor& wsub, at::Tensor& dx, int64_t a, int64_t b, int64_t cfg) {
+  TORCH_CHECK(!damd_conv_cfg_is_sk(static_cast<int>(cfg)) && conv_supported(dy, wsub, cfg, 1, 0),
+              "conv_dgrad_phase: unsupported input / weight / config");
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kBFloat16 && dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              dx.size(0) == dy.size(0) && dx.size(1) == wsub.size(0) && dx.size(2) == 2 * dy.size(2) &&
+              dx.size(3) == 2 * dy.size(3) && wsub.size(2) <= 2 && wsub.size(3) <= 2 && (a | b) >= 0 && a < 2 && b < 2,
+              "conv_dgrad_phase: bad geometry");
+  const int64_t N = dy.size(0), K = dy.size(1), H = dy.size(2), W = dy.size(3), C = wsub.size(0);
+  TORCH_CHECK(N * 4 * H * W < (int64_t{1} << 31) - 4096, "conv_dgrad_phase: tensor too large");
+  auto wl = wsub.contiguous(at::MemoryFormat::ChannelsLast);
+  const int G = damd_conv_groups(N * H * W, static_cast<int>(C), static_cast<int>(W), static_cast<int>(cfg), 0);
+  const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dx.data_ptr(), nullptr, static_cast<int>(N),
+                                      static_cast<int>(H), static_cast<int>(W), static_cast<int>(K), static_cast<int>(C),
+                                      static_cast<int>(wsub.size(2)), static_cast<int>(wsub.size(3)), 1, 0,
+                                      static_cast<int>(cfg), G, cur_stream(), 0, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr, 0, 4 | static_cast<int>(a << 1) | static_cast<int>(b));
+  TORCH_CHECK(rc == 0, "conv_dgrad_phase: launch rejected");
+}
+
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  bool want_stats, int64_t cfg, int64_t groups) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
@@ -1335,6 +1359,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
   m.def("conv_sk_timeouts", &conv_sk_timeouts, py::arg("like"), py::arg("reset") = false);
+  m.def("conv_dgrad_phase", &conv_dgrad_phase);
   m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });
   m.def("wgrad_num_cfgs", &damd_wgrad_num_cfgs);
   m.def("wgrad_supported", &wgrad_supported);

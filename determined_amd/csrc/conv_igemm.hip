@@ -55,7 +55,19 @@ struct Geo {
   int cblk;          // C / 64
   int ksteps;        // R * S * cblk
   int ptiles, ctiles, groups;
+  // output placement: ost == 0 -> output pixel m is row m of y; ost == 2 -> y is an
+  // [N][OHf][OWf] grid and output pixel m = (n, i, j) of the OH x OW grid goes to (n, 2i + oa, 2j + ob)
+  // (one phase of a stride-2 input gradient, conv_phase_launch)
+  int ost, oa, ob, OHf, OWf;
 };
+
+__device__ __forceinline__ int64_t out_row(const Geo& g, int64_t m) {
+  if (g.ost == 0) return m;
+  const uint32_t u = static_cast<uint32_t>(m), t = u / static_cast<uint32_t>(g.OW);
+  const uint32_t j = u - t * static_cast<uint32_t>(g.OW), n = t / static_cast<uint32_t>(g.OH);
+  const uint32_t i = t - n * static_cast<uint32_t>(g.OH);
+  return (static_cast<int64_t>(n) * g.OHf + 2 * i + g.oa) * g.OWf + 2 * j + g.ob;
+}
 
 __device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
@@ -211,7 +223,7 @@ __device__ __forceinline__ void epi_store_tile(const f4 (&acc)[FI][FJ], int64_t 
           v.v[e] = pk[0]; v.v[e + 1] = pk[1];
         }
         if (ok) {
-          *reinterpret_cast<bf16x8*>(y + m * g.K + co) = v;
+          *reinterpret_cast<bf16x8*>(y + out_row(g, m) * g.K + co) = v;
           if (EPI == kEpiStats) {  // statistics of the fp32 conv outputs (before the bf16 store)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -774,7 +786,7 @@ constexpr int kHaloProRows = 6;  // register-staged halo rows per lane: HR <= 6 
 template <int BCO, int BP, int WCO, int NW, int EPI, int SK = 0, int PRO = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk, ProArgs pa) {
+               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk, ProArgs pa, int sch) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -976,26 +988,52 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     const bf16_t* sw = wts + (it % 3) * WSLOT;
     const bf16_t* sh = halo + (c_halo & 1) * HSLOT;
     const int rowoff = (c_tap / 3) * g.W + (c_tap % 3);
+    auto read_a = [&](int kk, int i) {
+      const int row = wco0 + a_row(i, rho);
+      return *reinterpret_cast<const s8*>(sw + row * kBK + (((kk * 4 + lg) ^ swz(row)) << 3));
+    };
+    auto read_b = [&](int kk, int j) {
+      const int row = wp0 + 16 * j + rho + rowoff;
+      return *reinterpret_cast<const s8*>(sh + row * kBK + (((kk * 4 + lg) ^ (row & 7)) << 3));
+    };
+    if (sch == 1) {  // both k-halves' fragment reads first: the second half's reads overlap the first's MFMAs
+      s8 a[2][FI], b[2][FJ];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + lg;
-      s8 a[FI], b[FJ];
+      for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        const int row = wco0 + a_row(i, rho);
-        a[i] = *reinterpret_cast<const s8*>(sw + row * kBK + ((chunk ^ swz(row)) << 3));
+        for (int i = 0; i < FI; ++i) a[kk][i] = read_a(kk, i);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) b[kk][j] = read_b(kk, j);
       }
+      if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half of each SIMD pair
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        const int row = wp0 + 16 * j + rho + rowoff;
-        const s8 v = *reinterpret_cast<const s8*>(sh + row * kBK + ((chunk ^ (row & 7)) << 3));
-        const bool ok = (vm[j] >> c_tap) & 1u;
-        b[j] = ok ? v : s8{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          if (!((vm[j] >> c_tap) & 1u)) b[kk][j] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
       }
+      if (wave >= NW / 2) __builtin_amdgcn_s_setprio(0);
+    } else {
 #pragma unroll
-      for (int i = 0; i < FI; ++i)
+      for (int kk = 0; kk < 2; ++kk) {
+        s8 a[FI], b[FJ];
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        for (int i = 0; i < FI; ++i) a[i] = read_a(kk, i);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          const s8 v = read_b(kk, j);
+          const bool ok = (vm[j] >> c_tap) & 1u;
+          b[j] = ok ? v : s8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+      }
     }
     if (++c_tap == 9) {
       c_tap = 0;
@@ -1628,6 +1666,7 @@ int64_t damd_conv_sk_ws_floats(int K, int W, int cfg) {
 }
 int damd_conv_sk_flag_words() { return kSkMaxBlocks + 16; }
 int damd_conv_cfg_is_sk(int cfg) { return cfg >= 0 && cfg < kNumCfgs && kCfgs[cfg].sk; }
+int c_is_sk(int cfg) { return damd_conv_cfg_is_sk(cfg); }
 
 // Heuristic default config for a layer: widest co tile the channel count allows.
 int damd_conv_default_cfg(int K, int64_t M) {
@@ -1649,6 +1688,15 @@ int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, 
   if (c.nst == 0)
     return R == 3 && S == 3 && stride == 1 && pad == 1 && W >= 1 && halo_lds_bytes(c, W) <= kHaloMaxLds;
   return 1;
+}
+
+// DAMD_HALO_SCH=1: the 3x3 halo kernel's all-reads-first k-step schedule (A/B switch)
+int halo_sch() {
+  static const int v = [] {
+    const char* e = getenv("DAMD_HALO_SCH");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 // DAMD_CONV_OVERSUB=k: k x the resident grid for the (non-stream-K) persistent configs, so blocks
@@ -1702,7 +1750,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
                          const void* d2, const void* yb, const uint8_t* mask, const float* mean,
                          const float* scale, const float* shift, int pro, const void* p_res, const float* p_scale,
                          const float* p_shift, const float* p_rscale, void* p_aout, uint8_t* p_mout, float* sk_ws,
-                         int* sk_flags, int d2hw) {
+                         int* sk_flags, int d2hw, int ophase) {
   if (!damd_conv_supported(C, K, R, S, stride, pad, W, cfg)) return -1;
   if (pro < 0 || pro > 2) return -4;
   if (pro && (!damd_conv_pro_supported_w(C, K, R, S, stride, pad, W, cfg) || p_scale == nullptr || p_shift == nullptr ||
@@ -1718,12 +1766,19 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
   g.OH = (H + 2 * pad - R) / stride + 1;
   g.OW = (W + 2 * pad - S) / stride + 1;
+  if (ophase != 0) {  // one phase of a stride-2 input gradient: output grid = input grid (taps 0 / +1)
+    if (stride != 1 || pad != 0 || R > 2 || S > 2 || epi != 0 || pro != 0 || c_is_sk(cfg)) return -6;
+    g.OH = H;
+    g.OW = W;
+  }
   g.M = static_cast<int64_t>(N) * g.OH * g.OW;
   g.cblk = C / kBK;
   g.ksteps = R * S * g.cblk;
   g.ptiles = static_cast<int>((g.M + c.bp - 1) / c.bp);
   g.ctiles = K / c.bco;
   g.groups = groups;
+  g.ost = ophase != 0 ? 2 : 0; g.oa = (ophase >> 1) & 1; g.ob = ophase & 1;
+  g.OHf = ophase != 0 ? 2 * g.OH : g.OH; g.OWf = ophase != 0 ? 2 * g.OW : g.OW;
   if (c.sk && (sk_ws == nullptr || sk_flags == nullptr || groups != damd_conv_groups(g.M, K, W, cfg, 0))) return -5;
   const SkArgs ska{sk_ws, sk_flags, sk_flags + kSkMaxBlocks};
   EpiArgs ea{static_cast<const bf16_t*>(d2), static_cast<const bf16_t*>(yb), mask, mean, scale, shift, d2hw >> 16,
@@ -1764,7 +1819,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   do {                                                                                                       \
     auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_, P_>;                                                  \
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa);              \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa, halo_sch());  \
   } while (0)
 #define H1(BCO, BP, WCO, NW, E, K_)                        \
   do {                                                     \

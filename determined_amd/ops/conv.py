@@ -264,6 +264,12 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
                                                    [0, 0], 1, [True, False, False])[0]
 
     k = w.shape[2]
+    if stride == 2 and k == 3 and pad == 1 and w.shape[3] == 3 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0:
+        cands = {"miopen": miopen}
+        for c in _phase_cfgs(e, dy, w):
+            cands[f"p{c}"] = (lambda c=c: _dgrad_s2_phases(e, dy, w, x.shape, c))
+        key = ("dgrad", tuple(dy.shape), tuple(w.shape), stride, pad)
+        return cands[_pick(key, cands, default="miopen")]()
     if stride != 1 or 2 * pad != k - 1:
         return miopen()
     wt = _flip_weight(w)
@@ -281,6 +287,39 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
         cands["gemm"] = gemm
     key = ("dgrad", tuple(dy.shape), tuple(w.shape), stride, pad)
     return cands[_pick(key, cands, default=next(iter(cands)))]()
+
+
+# stride-2 3x3 input gradient by phases: dX[2i+a, 2j+b] only sees the taps r with (2i+a+1-r) even --
+# a=0: r=1 at dY row i; a=1: r=2 at row i and r=0 at row i+1 (likewise for columns).  Each of the
+# four phases is a stride-1 pad-0 conv of dY with a 1x1 / 1x2 / 2x1 / 2x2 sub-kernel whose epilogue
+# writes its pixels of dX directly (conv_igemm.hip Geo::ost): 9 taps of MFMA work in all instead of
+# the 36 of a zero-inserted dense dgrad, and no zero fill.
+_PHASE_TAPS = {0: [1], 1: [2, 0]}  # tap index (r or s) per offset dh = 0, +1
+
+
+def _phase_weights(w: torch.Tensor):
+    ws = []
+    for a in (0, 1):
+        for b in (0, 1):
+            sub = w[:, :, _PHASE_TAPS[a]][:, :, :, _PHASE_TAPS[b]]  # [K][C][Rp][Sp]
+            ws.append(((a, b), sub.transpose(0, 1).contiguous(memory_format=torch.channels_last)))
+    return ws
+
+
+def _phase_cfgs(e, dy: torch.Tensor, w: torch.Tensor):
+    if not hasattr(e, "conv_dgrad_phase") or dy.dtype != torch.bfloat16 or not dy.is_contiguous(
+            memory_format=torch.channels_last):
+        return []
+    probe = w[:, :, :2, :2].transpose(0, 1).contiguous(memory_format=torch.channels_last)
+    return [c for c in range(e.conv_num_cfgs())
+            if not e.conv_sk_cfg(c) and e.conv_supported(dy, probe, c, 1, 0) and _allowed("dgrad_phase", c)]
+
+
+def _dgrad_s2_phases(e, dy: torch.Tensor, w: torch.Tensor, xshape, cfg: int) -> torch.Tensor:
+    dx = torch.empty(xshape, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+    for (a, b), sub in _phase_weights(w):
+        e.conv_dgrad_phase(dy, sub, dx, a, b, cfg)
+    return dx
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:

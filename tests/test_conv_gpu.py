@@ -154,3 +154,25 @@ def test_conv3x3_halo_wgrad_matches_fp32(ext, shape):
         torch.testing.assert_close(dw32, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
         ran += 1
     assert ran > 0
+
+
+@pytest.mark.parametrize("shape", [(8, 128, 128, 56), (4, 256, 256, 28), (4, 512, 512, 14), (2, 64, 128, 16)])
+def test_stride2_3x3_dgrad_by_phases(ext, shape):
+    """The four-phase stride-2 3x3 input gradient (ops/conv.py _dgrad_s2_phases) against an fp32
+    reference, for every tile config that supports the phase geometry."""
+    from determined_amd.ops import conv as C
+
+    n, cin, cout, hw = shape
+    g = torch.Generator(device="cuda")
+    g.manual_seed(hw)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, hw // 2, hw // 2, device="cuda", generator=g).to(torch.bfloat16)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w.float(), dy.float(), stride=2, padding=1)
+    cfgs = C._phase_cfgs(ext, dy, w)
+    assert cfgs
+    for c in cfgs:
+        dx = C._dgrad_s2_phases(ext, dy, w, (n, cin, hw, hw), c)
+        err = ((dx.float() - ref).norm() / ref.norm()).item()
+        assert err < 1e-2, (c, err)
