@@ -110,6 +110,7 @@ def _parse_exclude(spec: str) -> frozenset:
 
 
 _EXCLUDE = _parse_exclude(os.environ.get("DAMD_CONV_EXCLUDE", ""))
+_PRO_ALWAYS_1X1 = os.environ.get("DAMD_PRO_ALWAYS_1X1", "0") == "1"
 
 
 def _allowed(kind: str, cfg: object) -> bool:
@@ -131,13 +132,15 @@ def exclude_stream_k() -> None:
 
 def _prologue_pays(key: tuple, t_fused: Callable[[], float], t_plain: Callable[[], float]) -> bool:
     """Whether a BN apply fused into a conv's operand staging beats the separate apply pass plus
-    the conv's best plain config for this layer (timed once, like the tile choice).  The 1x1
-    prologues always win (measured); the 3x3 halo prologue re-stages its halo per co tile and only
-    pays on some layers."""
+    the conv's best plain config for this layer (timed once, like the tile choice).  The staging
+    is redone for every output-channel tile, so it pays where there are few co tiles and many
+    pixels (the 56x56 / 28x28 layers) and loses on the 7x7 layers with 2048 channels (8 co tiles)."""
     global _DB_LOADED
     if not _DB_LOADED:
         _DB_LOADED = True
         load_tune_db()
+    if _PRO_ALWAYS_1X1 and len(key) > 2 and len(key[2]) == 4 and key[2][2] == 1:
+        return True  # A/B switch: the round-2 behaviour (1x1 prologues never timed)
     got = _TUNE.get(key)
     if got is None:
         got = bool(_TUNE_ON and not torch.cuda.is_current_stream_capturing() and t_fused() < t_plain())
@@ -388,6 +391,12 @@ class _StridedGrad:
         return full
 
 
+def _compact_like(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """A shape-only stand-in for a stride-2 1x1 conv's input on its output grid (timing only)."""
+    return torch.empty((x.shape[0], x.shape[1]) + tuple(g.shape[2:]), device=x.device, dtype=x.dtype,
+                       memory_format=torch.channels_last)
+
+
 class _IGemmConvFn(torch.autograd.Function):
     """Forward on conv_igemm.hip (+ BN statistic partials); backward: input gradient by
     :func:`_dgrad`, weight gradient by :func:`_wgrad`.  ``compact_dx``: a 1x1 stride-2 conv whose
@@ -418,6 +427,19 @@ class _IGemmConvFn(torch.autograd.Function):
             cfgs = ([c for c in range(e.conv_num_cfgs())
                      if e.conv_pro_supported(parked.dz, wt, c) and _allowed("dgrad_pro2", c)]
                     if weight.shape[2] == 1 and weight.shape[3] == 1 and pad == 0 and ctx.needs_input_grad[0] else [])
+            if cfgs:  # fused only where it times faster than the apply pass + the plain input gradient
+                def t_fused() -> float:
+                    return min(_time_once(lambda c=c: e.conv_fwd_pro2(parked.dz, wt, parked.y, parked.coef, c))
+                               for c in cfgs)
+
+                def t_plain() -> float:
+                    g = parked.materialise()
+                    return _time_once(parked.materialise) + _time_once(lambda: _dgrad(g, x if stride == 1 else
+                                                                                   _compact_like(x, g), weight, 1, 0))
+
+                if not _prologue_pays(("dgrad_pro2_pays", tuple(parked.dz.shape), tuple(weight.shape)), t_fused,
+                                      t_plain):
+                    cfgs = []
             if cfgs:  # dX with dy = A*dz + B*y + Cc formed in the operand staging; dy returned for dW
                 cands = {c: (lambda c=c: e.conv_fwd_pro2(parked.dz, wt, parked.y, parked.coef, c)) for c in cfgs}
                 key = ("dgrad_pro2", tuple(parked.dz.shape), tuple(weight.shape))
@@ -638,7 +660,7 @@ class _BNActConvFn(torch.autograd.Function):
             if _prologue_pays(key, t_fused, t_plain):
                 fused_bwd = fused_fn()
                 parked = None
-        if parked is not None and pro_cfgs and k != 1:
+        if parked is not None and pro_cfgs and fused_bwd is None:  # 1x1 and 3x3: fused only where it pays
             dzn, yn, coef = parked.dz, parked.y, parked.coef
             plain_cfgs = _igemm_cfgs(e, dzn, wt, 1, k - 1 - pad)
 
@@ -738,20 +760,25 @@ def bn_act_conv(bn: nn.Module, y: torch.Tensor, stats_part: Optional[torch.Tenso
                     if stats_part is not None and ops.fusion_enabled("bn_prologue") and st == 1
                     and 2 * pad == w.shape[2] - 1
                     and (residual is None or w.shape[2] == 1) else [])  # 3x3 prologue: no residual
-        if pro_cfgs and w.shape[2] != 1:
+        if pro_cfgs:  # the fused apply re-stages the operand per co tile: time it against the apply pass
             def t_fused() -> float:  # (only runs when the choice is not cached yet)
                 dummy = torch.zeros(4, y.shape[1], device=y.device, dtype=torch.float32)
                 dummy[2].fill_(1.0)
-                return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, None, dummy, False, c, None)) for c in pro_cfgs)
+                return min(_time_once(lambda c=c: e.conv_bnact_fwd(y, w, rt, dummy, rt is not None, c, None))
+                           for c in pro_cfgs)
 
             def t_plain() -> float:
-                apply = (lambda: e.bn_act_fwd(y, bn.weight, bn.bias, None, None, 0.0, float(bn.eps), None, True, True,
+                apply = (lambda: e.bn_act_fwd(y, bn.weight, bn.bias, None, None, 0.0, float(bn.eps), rt, True, True,
                                               stats_part))
                 a0 = apply()[0]
-                return _time_once(apply) + min(_time_once(lambda c=c: e.conv_fwd(a0, w, st, pad, True, c, 0))
-                                               for c in _igemm_cfgs(e, a0, w, st, pad))
+                t = _time_once(apply) + min(_time_once(lambda c=c: e.conv_fwd(a0, w, st, pad, True, c, 0))
+                                            for c in _igemm_cfgs(e, a0, w, st, pad))
+                if lres is not None:  # the plain path also materialises the shortcut BN (no stats update here)
+                    t += _time_once(lambda: e.bn_act_fwd(lres.y, lres.bn.weight, lres.bn.bias, None, None, 0.0,
+                                                         float(lres.bn.eps), None, False, False, lres.part))
+                return t
 
-            if not _prologue_pays(("fwd_pro_pays", tuple(y.shape), tuple(w.shape)), t_fused, t_plain):
+            if not _prologue_pays(("fwd_pro_pays", tuple(y.shape), tuple(w.shape), rt is not None), t_fused, t_plain):
                 pro_cfgs = []
         if lres is not None and not (pro_cfgs and w.shape[2] == 1):  # no 1x1 prologue to fold it into
             residual, lres = lres.materialise(), None
