@@ -452,7 +452,7 @@ __device__ __forceinline__ void sk_gather(f4 (&acc)[FI][FJ], const SkArgs& sk, c
 
 // SCH (k-step schedule): 0 = per 32-deep half: fragment reads then its MFMAs; 1 = all fragment
 // reads of the k-step issued first (the second half's reads overlap the first half's MFMAs);
-// 2 = as 1 with s_setprio(1) over the MFMA block.
+// 2 = as 1 with s_setprio(1) over the MFMA block; 3 = software-pipelined across k-steps (below).
 template <int BCO, int BP, int WCO, int NW, int NST, int EPI, int SCH = 0, int PRO = 0, int SK = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
@@ -468,7 +468,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   constexpr int NIW = BCO / (8 * NW), NIX = BP / (8 * NW);  // DMA instructions per wave per stage
   constexpr int NL = NIW + NIX;
   static_assert(NL * (NST - 2) <= 63, "vmcnt range");
-  static_assert(!PRO || (NST == 3 && SCH == 0), "prologue mode uses the 3-slot ring");
+  static_assert(!PRO || (NST == 3 && (SCH == 0 || SCH == 3)), "prologue mode uses the 3-slot ring");
   // one LDS array (a second __shared__ object makes hipcc wait for every DMA before each
   // ds_read): NST ring slots, then the block's per-channel BN parameters for the BN-backward
   // epilogues (mean, scale, shift of its BCO output channels; the co tile is fixed per block)
@@ -678,70 +678,62 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
   }
 
-  if (PRO) {
-    // item j: weights DMA + input rows to registers at iteration j-2, transform into LDS at
-    // iteration j-1, MFMAs at iteration j
+  if constexpr (SCH == 3) {
+    // Software-pipelined k-steps: the fragments of each k-half are read from LDS while the other
+    // half's MFMAs run -- the item's second half during its first half's MFMAs, the NEXT item's
+    // first half (after the one barrier per item, placed mid-item) during this item's second
+    // half.  The MFMA pipe then waits on LDS only at the start of a launch, not at every k-step.
+    // Ring safety: the barrier of iteration it follows every wave's wait on its reads of slot it
+    // (lgkmcnt) and on the DMA / operand registers of item it+1 (vmcnt), so item it+2 may then be
+    // issued into slot (it+2) % NST and item it+1's operand stored (PRO) into slot (it+1) % NST.
+    s8 fa[2][FI], fb[2][FJ];
+    auto read_half = [&](int slot, int kk) {
+      const bf16_t* sw = lds + slot * STAGE;
+#pragma unroll
+      for (int i = 0; i < FI; ++i) fa[kk][i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) fb[kk][j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
+    };
+    auto mfma_half = [&](int kk) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[kk][i], fb[kk][j], acc[i][j]);
+    };
     if (items > 0) {
       issue(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store_px(0);
-    }
-    if (items > 1) issue(1);
-  } else {
-#pragma unroll
-    for (int s0 = 0; s0 < NST - 1; ++s0)
-      if (s0 < items) issue(s0);
-  }
-  Cursor cc{0, 0, 0, 0, 0};
-  seg_enter(cc, plan, g.ksteps);
-  for (int it = 0; it < items; ++it) {
-    if (PRO) {
-      // weights of item it, input registers of item it+1 and this wave's LDS writes of item it
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (PRO) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_px(0);
+        if (items > 1) issue(1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        if (items > 1) {
+          issue(1);
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
       __builtin_amdgcn_s_barrier();
-      if (it + 1 < items) store_px((it + 1) % NST);
-      if (it + 2 < items) issue((it + 2) % NST);
-    } else {
-      // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
-      const int ahead = items - 1 - it;
-      if (NST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
-      else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
-      if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+      asm volatile("" ::: "memory");
+      read_half(0, 0);
     }
-    const bf16_t* sw = lds + (it % NST) * STAGE;
-    if (SCH == 0) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        s8 a[FI], b[FJ];
-#pragma unroll
-        for (int i = 0; i < FI; ++i) a[i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) b[j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    Cursor cc{0, 0, 0, 0, 0};
+    seg_enter(cc, plan, g.ksteps);
+    for (int it = 0; it < items; ++it) {
+      read_half(it % NST, 1);
+      mfma_half(0);
+      if (it + 1 < items) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // item it+1: DMA (+ operand registers, PRO)
+        if (PRO) store_px((it + 1) % NST);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot it (+ its stores)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + 2 < items) issue((it + 2) % NST);
+        read_half((it + 1) % NST, 0);
       }
-    } else {
-      s8 a[2][FI], b[2][FJ];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int i = 0; i < FI; ++i) a[kk][i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) b[kk][j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
-      }
-      if (SCH == 2) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
-      if (SCH == 2) __builtin_amdgcn_s_setprio(0);
-    }
+      mfma_half(1);
     if (++cc.k == cc.kend) {
       const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
       if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
@@ -755,6 +747,87 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 #pragma unroll
         for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
       seg_next(cc, plan, g.ksteps);
+    }
+    }
+  } else {
+    if (PRO) {
+      // item j: weights DMA + input rows to registers at iteration j-2, transform into LDS at
+      // iteration j-1, MFMAs at iteration j
+      if (items > 0) {
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_px(0);
+      }
+      if (items > 1) issue(1);
+    } else {
+  #pragma unroll
+      for (int s0 = 0; s0 < NST - 1; ++s0)
+        if (s0 < items) issue(s0);
+    }
+    Cursor cc{0, 0, 0, 0, 0};
+    seg_enter(cc, plan, g.ksteps);
+    for (int it = 0; it < items; ++it) {
+      if (PRO) {
+        // weights of item it, input registers of item it+1 and this wave's LDS writes of item it
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (it + 1 < items) store_px((it + 1) % NST);
+        if (it + 2 < items) issue((it + 2) % NST);
+      } else {
+        // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
+        const int ahead = items - 1 - it;
+        if (NST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
+        else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
+        if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+      }
+      const bf16_t* sw = lds + (it % NST) * STAGE;
+      if (SCH == 0) {
+  #pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          s8 a[FI], b[FJ];
+  #pragma unroll
+          for (int i = 0; i < FI; ++i) a[i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
+  #pragma unroll
+          for (int j = 0; j < FJ; ++j) b[j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
+  #pragma unroll
+          for (int i = 0; i < FI; ++i)
+  #pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        }
+      } else {
+        s8 a[2][FI], b[2][FJ];
+  #pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+  #pragma unroll
+          for (int i = 0; i < FI; ++i) a[kk][i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
+  #pragma unroll
+          for (int j = 0; j < FJ; ++j) b[kk][j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
+        }
+        if (SCH == 2) __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+  #pragma unroll
+          for (int i = 0; i < FI; ++i)
+  #pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
+        if (SCH == 2) __builtin_amdgcn_s_setprio(0);
+      }
+      if (++cc.k == cc.kend) {
+        const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
+        if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
+          sk_publish<FI, FJ, NT>(acc, sk, rid);
+        } else {
+          if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.ksteps, g.ctiles, ct);
+          epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, cc.pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+        }
+  #pragma unroll
+        for (int i = 0; i < FI; ++i)
+  #pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        seg_next(cc, plan, g.ksteps);
+      }
     }
   }
 
@@ -1632,7 +1705,9 @@ constexpr Cfg kCfgs[] = {{64, 128, 1, 4, 2, 0},  {128, 128, 2, 4, 2, 0}, {64, 25
                          // 14-21: stream-K work split of the generic / halo tiles above (make_plan)
                          {128, 128, 2, 4, 2, 0, 1}, {256, 128, 4, 8, 3, 0, 1}, {128, 256, 2, 8, 3, 0, 1},
                          {64, 256, 1, 8, 3, 0, 1},  {128, 256, 2, 8, 0, 0, 1}, {64, 256, 1, 8, 0, 0, 1},
-                         {128, 128, 2, 4, 0, 0, 1}, {256, 128, 4, 8, 0, 0, 1}};
+                         {128, 128, 2, 4, 0, 0, 1}, {256, 128, 4, 8, 0, 0, 1},
+                         // 22-25: software-pipelined k-steps (SCH 3) of the generic tiles
+                         {128, 128, 2, 4, 2, 3}, {256, 128, 4, 8, 3, 3}, {128, 256, 2, 8, 3, 3}, {64, 256, 1, 8, 3, 3}};
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
@@ -1732,7 +1807,7 @@ int damd_conv_pro_supported(int C, int K, int R, int S, int stride, int pad, int
   if (c.nst == 0)  // 3x3 halo kernel: the 64-channel / 256-pixel 8-wave tiles (register-staged halo)
     return c.bco == 64 && c.bp == 256 && c.nw == 8 && R == 3 && S == 3 && stride == 1 && pad == 1 &&
            damd_conv_supported(C, K, R, S, stride, pad, 1, cfg);
-  return c.nst == 3 && c.sch == 0 && R == 1 && S == 1 && stride == 1 && pad == 0 &&
+  return c.nst == 3 && (c.sch == 0 || c.sch == 3) && R == 1 && S == 1 && stride == 1 && pad == 0 &&
          damd_conv_supported(C, K, R, S, stride, pad, 1, cfg);
 }
 
@@ -1790,13 +1865,13 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   bf16_t* yp = static_cast<bf16_t*>(y);
 #define L1(BCO, BP, WCO, NW, NST, E, SC, K_)                                                              \
   do {                                                                                                     \
-    if constexpr (NST == 3 && SC == 0) {                                                                   \
+    if constexpr (NST == 3 && (SC == 0 || SC == 3)) {                                                      \
       if (pro == 1) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 1, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 1, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
       if (pro == 2) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, 0, 2, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
+        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 2, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
     }                                                                                                      \
@@ -1861,7 +1936,11 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
     case 18: HK(128, 256, 2, 8, 1); break;
     case 19: HK(64, 256, 1, 8, 1); break;
     case 20: HK(128, 128, 2, 4, 1); break;
-    default: HK(256, 128, 4, 8, 1); break;
+    case 21: HK(256, 128, 4, 8, 1); break;
+    case 22: LS(128, 128, 2, 4, 2, 3); break;
+    case 23: LS(256, 128, 4, 8, 3, 3); break;
+    case 24: LS(128, 256, 2, 8, 3, 3); break;
+    default: LS(64, 256, 1, 8, 3, 3); break;
   }
 #undef L
 #undef LS
