@@ -109,7 +109,19 @@ void damd_bn_pool_bwd_launch(const void*, const uint8_t*, const void*, int64_t, 
                              const float*, const float*, const float*, float*, float*, void*, void*, void*, int, int,
                              hipStream_t, const void*, const void*);
 void damd_hw_broadcast_launch(const void*, void*, int64_t, int64_t, int, float, int, hipStream_t);
+void damd_stem_pool_bn_fwd_launch(const float*, int, int64_t, const void*, void*, int64_t, int, const void*,
+                                  const void*, float*, float*, float, float, float*, float*, float*, float*, int,
+                                  hipStream_t);
+void damd_stem_pool_bn_bwd_launch(const void*, const void*, const void*, const float*, const float*, const float*,
+                                  const float*, float*, float*, void*, void*, void*, int64_t, int64_t, int, int,
+                                  hipStream_t);
 // launchers (conv_stem.hip)
+extern "C" int damd_stem_pool_supported(int64_t, int64_t);
+extern "C" int damd_stem_pool_blocks(int64_t, int64_t, int64_t);
+extern "C" void damd_stem_pool_fwd_launch(const void*, const void*, const void*, int, void*, uint8_t*, float*, int64_t,
+                                          int, int, hipStream_t);
+extern "C" void damd_stem_pool_bwd_launch(const void*, const void*, const void*, const uint8_t*, const float*, float*,
+                                          void*, int, int64_t, int, int, hipStream_t);
 extern "C" int damd_stem_supported(int64_t, int64_t);
 extern "C" int damd_stem_fwd_blocks(int64_t, int);
 extern "C" void damd_stem_fwd_launch(const void*, const void*, void*, float*, int64_t, int, int, hipStream_t);
@@ -731,13 +743,17 @@ bool stem_conv_supported(const at::Tensor& x, const at::Tensor& w) {
          damd_stem_supported(x.size(2), x.size(3));
 }
 
+// [64][7][32] bf16 weight image: k' = 4*kw + ci with zero pad at kw = 7 / ci = 3 (28 KB)
+at::Tensor stem_weight_image(const at::Tensor& w) {
+  return at::constant_pad_nd(w.to(at::kBFloat16).permute({0, 2, 3, 1}), {0, 1, 0, 1}).reshape({64, 7, 32}).contiguous();
+}
+
 // returns (y, stats partials [nb, 2, 64] or an empty tensor) -- see conv_stem.hip
 std::vector<at::Tensor> stem_conv_fwd(const at::Tensor& x, const at::Tensor& w, bool want_stats) {
   TORCH_CHECK(stem_conv_supported(x, w), "stem_conv_fwd: unsupported input");
   const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
   const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  // [64][7][32] bf16 weight image: k' = 4*kw + ci with zero pad at kw = 7 / ci = 3 (28 KB)
-  auto wl = at::constant_pad_nd(w.to(at::kBFloat16).permute({0, 2, 3, 1}), {0, 1, 0, 1}).reshape({64, 7, 32}).contiguous();
+  auto wl = stem_weight_image(w);
   auto y = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor part = want_stats ? at::empty({damd_stem_fwd_blocks(N, static_cast<int>(H)), 2, 64},
                                           x.options().dtype(at::kFloat))
@@ -762,6 +778,97 @@ at::Tensor stem_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::
   damd_stem_wgrad_launch(x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), dtype_code(w), N,
                          static_cast<int>(H), static_cast<int>(W), cur_stream());
   return w.is_contiguous(at::MemoryFormat::ChannelsLast) ? dw : dw.contiguous();
+}
+
+// ---------------------------------------------------------------- fused stem: conv + BN + ReLU + max-pool
+// conv7x7/s2 -> BatchNorm (training statistics) -> ReLU -> maxpool3x3/s2/p1 without the conv's
+// full-size output (conv_stem.hip stem_pool_*).  gamma/beta: the BN affine parameters (bf16/fp32).
+bool stem_pool_supported(const at::Tensor& x, const at::Tensor& w) {
+  return stem_conv_supported(x, w) && damd_stem_pool_supported(x.size(2), x.size(3));
+}
+
+// returns (y [N, 64, PH, PW] channels-last, window positions uint8, stats [4, 64] (mean, invstd,
+// scale, shift), xarg: the raw conv value each window selected)
+std::vector<at::Tensor> stem_pool_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& gamma,
+                                      const at::Tensor& beta, const c10::optional<at::Tensor>& running_mean,
+                                      const c10::optional<at::Tensor>& running_var, double momentum, double eps) {
+  TORCH_CHECK(stem_pool_supported(x, w), "stem_pool_fwd: unsupported input");
+  TORCH_CHECK(gamma.numel() == 64 && beta.numel() == 64 && gamma.is_contiguous() && beta.is_contiguous() &&
+              gamma.scalar_type() == beta.scalar_type() &&
+              (gamma.scalar_type() == at::kBFloat16 || gamma.scalar_type() == at::kFloat),
+              "stem_pool_fwd: BN weight/bias must be 64-element bf16/fp32 tensors");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    TORCH_CHECK(running_mean->scalar_type() == at::kFloat && running_var->scalar_type() == at::kFloat,
+                "running stats must be float32");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, PH = OH / 2, PW = OW / 2;
+  auto wl = stem_weight_image(w);
+  const int nb = damd_stem_pool_blocks(N, H, W);
+  auto fopts = x.options().dtype(at::kFloat);
+  auto part = at::empty({nb, 2, 64}, fopts);
+  auto stats = at::empty({4, 64}, fopts);
+  auto xarg = at::empty({N, 64, PH, PW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto y = at::empty_like(xarg);
+  auto idx = at::empty({N * PH * PW * 64}, x.options().dtype(at::kByte));
+  TORCH_CHECK(N * PH * PW * 64 < (int64_t{1} << 31), "stem_pool_fwd: pooled tensor too large (32-bit indexing)");
+  damd_stem_pool_fwd_launch(x.data_ptr(), wl.data_ptr(), gamma.data_ptr(), dtype_code(gamma), xarg.data_ptr(),
+                            idx.data_ptr<uint8_t>(), part.data_ptr<float>(), N, static_cast<int>(H), static_cast<int>(W),
+                            cur_stream());
+  damd_stem_pool_bn_fwd_launch(part.data_ptr<float>(), nb, N * OH * OW, xarg.data_ptr(), y.data_ptr(), N * PH * PW, 64,
+                               gamma.data_ptr(), beta.data_ptr(), rm, rv, static_cast<float>(momentum),
+                               static_cast<float>(eps), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
+                               stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), dtype_code(gamma), cur_stream());
+  return {y, idx, stats, xarg};
+}
+
+// returns (dW in w's dtype / memory format, dgamma, dbeta); dp [+ dp2]: the pooled output's gradient(s)
+std::vector<at::Tensor> stem_pool_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dp,
+                                      const c10::optional<at::Tensor>& dp2, const at::Tensor& idx,
+                                      const at::Tensor& xarg, const at::Tensor& stats, const at::Tensor& gamma) {
+  TORCH_CHECK(stem_pool_supported(x, w), "stem_pool_bwd: unsupported input");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat, "stem_pool_bwd: weight dtype");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, PH = OH / 2, PW = OW / 2;
+  TORCH_CHECK(dp.dim() == 4 && dp.size(0) == N && dp.size(1) == 64 && dp.size(2) == PH && dp.size(3) == PW &&
+              dp.scalar_type() == at::kBFloat16 && dp.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              (reinterpret_cast<uintptr_t>(dp.data_ptr()) & 15) == 0,
+              "stem_pool_bwd: dp must be a [N, 64, PH, PW] bf16 channels-last tensor");
+  TORCH_CHECK(xarg.sizes() == dp.sizes() && xarg.strides() == dp.strides() && xarg.scalar_type() == at::kBFloat16,
+              "stem_pool_bwd: xarg must match dp");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == N * PH * PW * 64 && idx.is_contiguous(),
+              "stem_pool_bwd: bad window-position tensor");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.size(0) == 4 && stats.size(1) == 64 && stats.is_contiguous(),
+              "stem_pool_bwd: bad stats");
+  const void* d2 = nullptr;
+  if (dp2.has_value() && dp2->defined()) {
+    TORCH_CHECK(dp2->sizes() == dp.sizes() && dp2->strides() == dp.strides() && dp2->scalar_type() == dp.scalar_type() &&
+                dp2->device() == dp.device(), "stem_pool_bwd: dp2 must match dp");
+    d2 = dp2->data_ptr();
+  }
+  auto fopts = x.options().dtype(at::kFloat);
+  const int64_t Q = N * PH * PW;
+  auto part_r = at::empty({damd_bn_num_blocks(Q, 64), 2, 64}, fopts);
+  auto coef = at::empty({3, 64}, fopts);
+  auto dgamma = at::empty({64}, gamma.options());
+  auto dbeta = at::empty({64}, gamma.options());
+  auto dz = at::empty_like(dp);
+  damd_stem_pool_bn_bwd_launch(dp.data_ptr(), d2, xarg.data_ptr(), stats[0].data_ptr<float>(), stats[1].data_ptr<float>(),
+                               stats[2].data_ptr<float>(), stats[3].data_ptr<float>(), part_r.data_ptr<float>(),
+                               coef.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(), dz.data_ptr(), Q, N * OH * OW,
+                               64, dtype_code(gamma), cur_stream());
+  auto wl = stem_weight_image(w);
+  const int nbw = damd_stem_pool_blocks(N, H, W);
+  auto part_w = at::empty({nbw, 64, 7 * 32}, fopts);
+  auto dw = at::empty({64, 3, 7, 7}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  damd_stem_pool_bwd_launch(x.data_ptr(), wl.data_ptr(), dz.data_ptr(), idx.data_ptr<uint8_t>(), coef.data_ptr<float>(),
+                            part_w.data_ptr<float>(), dw.data_ptr(), dtype_code(w), N, static_cast<int>(H),
+                            static_cast<int>(W), cur_stream());
+  return {w.is_contiguous(at::MemoryFormat::ChannelsLast) ? dw : dw.contiguous(), dgamma, dbeta};
 }
 
 // ---------------------------------------------------------------- implicit-GEMM convolution
@@ -1368,6 +1475,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_supported", &stem_conv_supported);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
+  m.def("stem_pool_supported", &stem_pool_supported);
+  m.def("stem_pool_fwd", &stem_pool_fwd);
+  m.def("stem_pool_bwd", &stem_pool_bwd);
   m.doc() = "determined_amd CDNA4 HIP kernels";
   m.def("build_chunk_table", &build_chunk_table);
   m.def("chunk_entry_bytes", &chunk_entry_bytes);

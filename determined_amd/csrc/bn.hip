@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(kBNThreads)
 pooled_bn_bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ dp2, const T* __restrict__ xarg,
                             const float* __restrict__ mean, const float* __restrict__ scale,
                             const float* __restrict__ shift, int64_t Q, int C, int64_t rows_per_block,
-                            float* __restrict__ part) {
+                            float* __restrict__ part, T* __restrict__ dzout = nullptr) {
   const Geo geo_ = geo(C);
   const int tid = threadIdx.x;
   const int cg0 = geo_.TPR <= kBNThreads ? tid % geo_.TPR : tid;
@@ -520,12 +520,15 @@ pooled_bn_bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ dp2,
       V8<T>::ld(dp + off, d);
       if (dp2 != nullptr) add_v8(dp2 + off, d);
       V8<T>::ld(xarg + off, a);
+      float z[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float dz = (a[k] * sc[k] + sh[k]) > 0.f ? d[k] : 0.f;
+        z[k] = dz;
         s[k] += dz;
         sx[k] += dz * (a[k] - mu[k]);
       }
+      if (dzout != nullptr) V8<T>::st(dzout + off, z);  // the fused stem backward's routed gradient
     }
     for (int which = 0; which < 2; ++which) {
       float* v = which == 0 ? s : sx;
@@ -992,6 +995,50 @@ void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, in
   else
     hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift,
                        static_cast<float*>(y), idx, Vout, TPR, g, static_cast<float*>(xarg));
+  DAMD_CHECK_LAUNCH();
+}
+
+// Fused ResNet stem (conv_stem.hip stem_pool_*): the BN statistics come from the conv kernel
+// (part [nb][2][C], count M = conv output pixels); the apply runs on the pooled window values
+// xarg ([Q][C], Q = pooled pixels): y = relu(xarg * scale + shift), exactly the pooled output.
+void damd_stem_pool_bn_fwd_launch(const float* part, int nb, int64_t M, const void* xarg, void* y, int64_t Q, int C,
+                                  const void* w, const void* b, float* run_mean, float* run_var, float momentum,
+                                  float eps, float* mean, float* invstd, float* scale, float* shift, int w_dtype,
+                                  hipStream_t st) {
+  const dim3 fg((C + kFinCh - 1) / kFinCh);
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
+                       momentum, eps, static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var,
+                       mean, invstd, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
+                       momentum, eps, static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var,
+                       mean, invstd, scale, shift);
+  const int TPR = C / 8;
+  const int64_t V = Q * TPR;
+  hipLaunchKernelGGL((bn_apply_kernel<bf16_t, false, true>), dim3(apply_grid(V, TPR)), dim3(kBNThreads), 0, st,
+                     static_cast<const bf16_t*>(xarg), scale, shift, nullptr, static_cast<bf16_t*>(y), V, TPR, nullptr);
+  DAMD_CHECK_LAUNCH();
+}
+
+// Its backward statistics: the pooled-domain reduce over (dp [+ dp2], xarg), which also writes
+// the masked pooled gradient dz for the fused weight-gradient kernel; then A, B, Cc (count M).
+// part: [damd_bn_num_blocks(Q, C)][2][C].
+void damd_stem_pool_bn_bwd_launch(const void* dp, const void* dp2, const void* xarg, const float* mean,
+                                  const float* invstd, const float* scale, const float* shift, float* part,
+                                  float* coef, void* dgamma, void* dbeta, void* dz, int64_t Q, int64_t M, int C,
+                                  int w_dtype, hipStream_t st) {
+  int nb;
+  const int64_t rpb = rows_per_block_for(Q, C, &nb);
+  hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st,
+                     static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), static_cast<const bf16_t*>(xarg),
+                     mean, scale, shift, Q, C, rpb, part, static_cast<bf16_t*>(dz));
+  if (w_dtype == 1)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
+                       nb, C, M, mean, invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
+                       nb, C, M, mean, invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   DAMD_CHECK_LAUNCH();
 }
 

@@ -14,7 +14,7 @@ from torch import nn
 
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
 from determined_amd.ops import fusion_enabled
-from determined_amd.ops.conv import LazyBNResidual, _materialise, bn_act_conv, conv_bn_input, stem_conv2d
+from determined_amd.ops.conv import LazyBNResidual, _materialise, bn_act_conv, conv_bn_input, stem_bn_pool
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -181,14 +181,13 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        # stem BN + ReLU + max-pool in one fused kernel pair (ops/bn.py: forward_maxpool)
         # Every activation between blocks feeds two consumers (next conv1 + shortcut): producers
         # hand out split-gradient pairs so the backward sums the two gradients inside the BN
         # kernels instead of in separate elementwise adds (ops/bn.py).
-        # stem conv emits the BN batch-statistic partials from its epilogue (ops/conv.py)
         split = fusion_enabled("split_grad")
-        y, part = stem_conv2d(self.conv1, x, with_stats=True)
-        x = self.bn1.forward_maxpool(y, self.maxpool, split_grad=split, stats_part=part)
+        # stem conv + BN + ReLU + max-pool as one op: the conv's full-size output is never stored
+        # (ops/conv.py stem_bn_pool; fallback: stem conv with BN statistics + bn1.forward_maxpool)
+        x = stem_bn_pool(self.conv1, self.bn1, self.maxpool, x, split_grad=split)
         blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
         if fusion_enabled("bn_conv") and all(_chainable(b) for b in blocks):
             x = _chain_blocks(blocks, x, split)

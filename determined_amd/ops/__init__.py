@@ -55,7 +55,7 @@ _DISABLED = frozenset(f.strip() for f in os.environ.get("DAMD_DISABLE_FUSIONS", 
 
 def fusion_enabled(name: str) -> bool:
     """Model-level fusions can be switched off for A/B measurements with
-    ``DAMD_DISABLE_FUSIONS=stem_conv,stem_stats,split_grad,avgpool,igemm_conv,conv_stats,bn_conv,bn_prologue,bn_lazy_bwd,
+    ``DAMD_DISABLE_FUSIONS=stem_conv,stem_stats,stem_pool,split_grad,avgpool,igemm_conv,conv_stats,bn_conv,bn_prologue,bn_lazy_bwd,
     compact_shortcut_grad,bn_residual_fold`` (the replacement is the
     plain PyTorch / MIOpen composition, never a silent eager fallback of a kernel)."""
     return name not in _DISABLED

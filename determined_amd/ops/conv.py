@@ -78,6 +78,59 @@ def stem_conv2d(conv: nn.Conv2d, x: torch.Tensor, with_stats: bool = False):
     return (y, None) if with_stats else y
 
 
+class _StemPoolFn(torch.autograd.Function):
+    """``maxpool3x3s2p1(relu(bn(conv7x7s2(x))))`` -- the whole ResNet stem -- without the conv's
+    full-size output (csrc/conv_stem.hip ``stem_pool_*``): the forward pools the raw conv rows
+    on chip by the sign of the BN weight and writes the selected values + window positions; the
+    backward recomputes the conv rows and feeds the BN input gradient straight into the weight
+    gradient.  Reference: the stem of ``examples/computer_vision`` ResNets (torchvision
+    ``resnet50``: conv1 -> bn1 -> relu -> maxpool)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, momentum, eps, split=False):
+        from determined_amd import ops
+
+        y, idx, stats, xarg = ops.ext().stem_pool_fwd(x, weight, gamma, beta, running_mean, running_var,
+                                                      float(momentum), float(eps))
+        ctx.save_for_backward(x, weight, idx, stats, gamma, xarg)
+        ctx.set_materialize_grads(False)
+        if split:
+            return y, y.detach()
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, dy2=None):
+        from determined_amd import ops
+        from determined_amd.ops.bn import _sum_grads
+
+        x, weight, idx, stats, gamma, xarg = ctx.saved_tensors
+        dy, dy2 = _sum_grads(dy, dy2, torch.channels_last)
+        if dy is None:
+            return (None,) * 9
+        dw, dg, db = ops.ext().stem_pool_bwd(x, weight, dy, dy2, idx, xarg, stats, gamma)
+        return None, dw, dg, db, None, None, None, None, None
+
+
+def stem_bn_pool(conv: nn.Conv2d, bn: nn.Module, pool: nn.MaxPool2d, x: torch.Tensor, split_grad: bool = False):
+    """``pool(relu(bn(conv(x))))`` for the ResNet stem: one fused op (:class:`_StemPoolFn`) when
+    the conv is :func:`stem_fusable`, ``bn`` a training-mode ``BatchNormAct2d`` with ReLU and
+    ``pool`` the 3x3/s2/p1 max-pool; else the stem conv (+ its BN statistics) and
+    ``bn.forward_maxpool``.  ``split_grad``: return ``(y, y)`` handles (ops/bn.py)."""
+    from determined_amd import ops
+
+    fusable = (stem_fusable(conv, x) and ops.fusion_enabled("stem_pool") and getattr(bn, "act", False)
+               and bn.affine and bn.training and bn.track_running_stats and bn.num_batches_tracked is not None
+               and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
+               and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and not pool.return_indices
+               and _plain_module(bn) and _plain_module(pool) and bn.weight.dtype == bn.bias.dtype
+               and bn.weight.dtype in (torch.bfloat16, torch.float32) and bool(ops.ext().stem_pool_supported(x, conv.weight)))
+    if not fusable:
+        y, part = stem_conv2d(conv, x, with_stats=True)
+        return bn.forward_maxpool(y, pool, split_grad=split_grad, stats_part=part)
+    rm, rv, momentum = bn.train_step_args()
+    return _StemPoolFn.apply(x, conv.weight, bn.weight, bn.bias, rm, rv, momentum, bn.eps, split_grad)
+
+
 def _plain_module(conv: nn.Module) -> bool:
     """No forward hooks / pre-hooks / parametrizations: calling the kernels directly instead of
     ``conv(x)`` would silently skip them."""

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 
 from determined_amd.models.resnet import resnet18, resnet50
 from determined_amd.ops.bn import BatchNormAct2d, global_avg_pool
-from determined_amd.ops.conv import stem_conv2d, stem_fusable
+from determined_amd.ops.conv import stem_bn_pool, stem_conv2d, stem_fusable
 from determined_amd.ops.fused import linear_gelu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,6 +56,11 @@ def test_stem_conv_and_pool_fallbacks_are_exact():
     torch.testing.assert_close(y, conv(x))
     z = torch.randn(2, 16, 5, 3)
     torch.testing.assert_close(global_avg_pool(z), torch.flatten(F.adaptive_avg_pool2d(z, 1), 1))
+    bn, pool = BatchNormAct2d(64), torch.nn.MaxPool2d(3, 2, 1)
+    bn_ref = BatchNormAct2d(64)
+    out = stem_bn_pool(conv, bn, pool, x)  # CPU: the unfused composition, running stats updated once
+    torch.testing.assert_close(out, pool(bn_ref(conv(x))))
+    torch.testing.assert_close(bn.running_mean, bn_ref.running_mean)
 
 
 def test_linear_gelu_fallback_matches_composition():

@@ -315,6 +315,81 @@ def test_stem_conv_bn_stats_fusion():
     torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 64), (3, 96, 160), (2, 224, 224)])
+@pytest.mark.parametrize("pdtype", [torch.bfloat16, torch.float32])
+def test_stem_pool_fused_matches_reference(shape, pdtype):
+    """conv_stem.hip stem_pool_* (conv + BN + ReLU + max-pool, no full-size conv output) vs the fp32
+    PyTorch composition on the same bf16 data: output, running statistics and the gradients of
+    the conv weight and the BN affine parameters, with some BN weights negative (min-pool path)."""
+    import determined_amd.ops as ops
+    from determined_amd.ops.conv import _StemPoolFn, stem_bn_pool
+
+    torch.manual_seed(0)
+    N, H, W = shape
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().to(pdtype)
+    bn = ops.BatchNormAct2d(64).cuda().to(pdtype)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(64) * 0.5 + 0.2)  # ~1/3 negative
+        bn.bias.copy_(torch.randn(64) * 0.2)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = (torch.randn(N, 3, H, W, device="cuda") + 0.3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert ops.ext().stem_pool_supported(x, conv.weight)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    y = stem_bn_pool(conv, bn, pool, x)
+    assert y.grad_fn is not None and type(y.grad_fn).__name__ == _StemPoolFn.__name__ + "Backward"
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    gr = bn.weight.detach().float().requires_grad_(True)
+    br = bn.bias.detach().float().requires_grad_(True)
+    rmr, rvr = rm0.clone(), rv0.clone()
+    c = torch.nn.functional.conv2d(x.float(), wr, stride=2, padding=3)
+    c = c + (c.detach().to(torch.bfloat16).float() - c.detach())  # the kernel normalises bf16-rounded outputs
+    yr = pool(torch.relu(torch.nn.functional.batch_norm(c, rmr, rvr, gr, br, True, 0.1, bn.eps)))
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(bn.running_mean, rmr, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, rvr, rtol=1e-3, atol=1e-4)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    for got, ref in ((conv.weight.grad, wr.grad), (bn.weight.grad, gr.grad), (bn.bias.grad, br.grad)):
+        assert got.dtype == pdtype
+        rel = ((got.float() - ref).norm() / ref.norm()).item()
+        assert rel < 2e-2, rel
+
+
+def test_stem_pool_fused_matches_unfused_kernels():
+    """The fused stem against the separate stem conv + BN/ReLU/max-pool kernels it replaces (same
+    bf16 arithmetic up to pooling ties and the bf16 sum of the two consumers' gradients)."""
+    import determined_amd.ops as ops
+    from determined_amd.ops.conv import stem_bn_pool, stem_conv2d
+
+    torch.manual_seed(1)
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().to(torch.bfloat16)
+    bn_a = ops.BatchNormAct2d(64).cuda().to(torch.bfloat16)
+    bn_b = ops.BatchNormAct2d(64).cuda().to(torch.bfloat16)
+    with torch.no_grad():
+        w = torch.randn(64) * 0.5 + 0.3
+        bn_a.weight.copy_(w)
+        bn_b.weight.copy_(w)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(8, 3, 128, 128, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    conv_b = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().to(torch.bfloat16)
+    conv_b.load_state_dict(conv.state_dict())
+    ya, ya2 = stem_bn_pool(conv, bn_a, pool, x, split_grad=True)
+    yc, part = stem_conv2d(conv_b, x, with_stats=True)
+    yb, yb2 = bn_b.forward_maxpool(yc, pool, split_grad=True, stats_part=part)
+    torch.testing.assert_close(ya.float(), yb.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-4, atol=1e-5)
+    g1 = torch.randn_like(ya)
+    g2 = torch.randn_like(ya)
+    ((ya.float() * g1.float()).sum() + (ya2.float() * g2.float()).sum()).backward()
+    ((yb.float() * g1.float()).sum() + (yb2.float() * g2.float()).sum()).backward()
+    for a, b in ((conv.weight.grad, conv_b.weight.grad), (bn_a.weight.grad, bn_b.weight.grad),
+                 (bn_a.bias.grad, bn_b.bias.grad)):
+        rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+        assert rel < 1e-2, rel
+
+
 def test_linear_gelu_fused_matches_reference():
     """Fused GELU forward / GELU'+bias-gradient backward vs the fp32 PyTorch composition."""
     from determined_amd.ops.fused import linear_gelu
