@@ -213,6 +213,7 @@ PYBIND11_MODULE(_native, m) {
       .def("add_agent", &Scheduler::add_agent)
       .def("remove_agent", &Scheduler::remove_agent)
       .def("set_agent_enabled", &Scheduler::set_agent_enabled)
+      .def("set_slot_enabled", &Scheduler::set_slot_enabled)
       .def("add_request",
            [](Scheduler& s, const std::string& alloc_id, const std::string& job_id, int slots, int priority,
               double weight, int64_t order, bool preemptible, const std::vector<std::string>& excluded_agents) {
@@ -255,6 +256,10 @@ PYBIND11_MODULE(_native, m) {
                a["num_slots"] = kv.second.num_slots;
                a["slot_owner"] = kv.second.slot_owner;
                a["enabled"] = kv.second.enabled;
+               py::list dis;
+               for (int i = 0; i < kv.second.num_slots; ++i)
+                 if (kv.second.slot_disabled[i]) dis.append(i);
+               a["disabled_slots"] = dis;
                out[py::str(kv.first)] = a;
              }
              return out;

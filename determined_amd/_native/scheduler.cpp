@@ -11,7 +11,13 @@ namespace damd_native {
 
 int AgentState::empty() const {
   int n = 0;
-  for (const auto& o : slot_owner) n += o.empty() ? 1 : 0;
+  for (int i = 0; i < num_slots; ++i) n += free_slot(i) ? 1 : 0;
+  return n;
+}
+
+int AgentState::disabled() const {
+  int n = 0;
+  for (int i = 0; i < num_slots; ++i) n += (slot_disabled[i] && slot_owner[i].empty()) ? 1 : 0;
   return n;
 }
 
@@ -20,10 +26,15 @@ void Scheduler::add_agent(const std::string& id, int slots) {
   a.id = id;
   a.num_slots = slots;
   a.slot_owner.assign(slots, "");
+  a.slot_disabled.assign(slots, 0);
   auto it = agents_.find(id);
   if (it != agents_.end()) {
-    // re-registration keeps existing ownership where possible
-    for (int i = 0; i < std::min<int>(slots, it->second.num_slots); ++i) a.slot_owner[i] = it->second.slot_owner[i];
+    // re-registration keeps existing ownership (and disabled slots) where possible
+    for (int i = 0; i < std::min<int>(slots, it->second.num_slots); ++i) {
+      a.slot_owner[i] = it->second.slot_owner[i];
+      a.slot_disabled[i] = it->second.slot_disabled[i];
+    }
+    a.enabled = it->second.enabled;
     a.zero_slot_containers = it->second.zero_slot_containers;
   }
   agents_[id] = a;
@@ -45,6 +56,13 @@ void Scheduler::remove_agent(const std::string& id) {
 void Scheduler::set_agent_enabled(const std::string& id, bool enabled) {
   auto it = agents_.find(id);
   if (it != agents_.end()) it->second.enabled = enabled;
+}
+
+bool Scheduler::set_slot_enabled(const std::string& id, int slot, bool enabled) {
+  auto it = agents_.find(id);
+  if (it == agents_.end() || slot < 0 || slot >= it->second.num_slots) return false;
+  it->second.slot_disabled[slot] = enabled ? 0 : 1;
+  return true;
 }
 
 void Scheduler::add_request(const Request& r) { reqs_[r.alloc_id] = r; }
@@ -69,7 +87,7 @@ void Scheduler::set_weight(const std::string& job_id, double weight) {
 int Scheduler::total_slots() const {
   int n = 0;
   for (const auto& kv : agents_)
-    if (kv.second.enabled) n += kv.second.num_slots;
+    if (kv.second.enabled) n += kv.second.usable();
   return n;
 }
 
@@ -83,7 +101,7 @@ int Scheduler::used_slots() const {
 double Scheduler::score(const Request& r, const AgentState& a) const {
   if (a.used() != 0 || r.slots != 0) {
     if (fit_ == Fit::Best) return 1.0 / (1.0 + a.empty());
-    return a.num_slots ? static_cast<double>(a.empty()) / a.num_slots : 0.0;
+    return a.usable() ? static_cast<double>(a.empty()) / a.usable() : 0.0;
   }
   return fit_ == Fit::Best ? 1.0 / (1.0 + a.zero_slot_containers) : 1.0 / (1.0 + a.zero_slot_containers);
 }
@@ -111,7 +129,7 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
   if (best) {
     std::vector<int> slots;
     for (int i = 0; i < best->num_slots && static_cast<int>(slots.size()) < r.slots; ++i)
-      if (best->slot_owner[i].empty()) slots.push_back(i);
+      if (best->free_slot(i)) slots.push_back(i);
     out->assignment.emplace_back(best->id, slots);
     return true;
   }
@@ -119,7 +137,8 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
   std::map<int, std::vector<const AgentState*>, std::greater<int>> by_slots;
   for (const auto& kv : agents) {
     const AgentState& a = kv.second;
-    if (!a.enabled || a.used() != 0 || a.num_slots == 0 || excluded(a.id)) continue;
+    // whole-agent fits use every slot of the agent: agents with disabled slots only take shared fits
+    if (!a.enabled || a.used() != 0 || a.num_slots == 0 || a.disabled() != 0 || excluded(a.id)) continue;
     by_slots[a.num_slots].push_back(&a);
   }
   for (auto& g : by_slots) {

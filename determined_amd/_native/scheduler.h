@@ -23,10 +23,14 @@ struct AgentState {
   std::string id;
   int num_slots = 0;
   std::vector<std::string> slot_owner;  // allocation id or "" per slot
+  std::vector<char> slot_disabled;      // `det slot disable` (reference agentrm slot enable/disable)
   int zero_slot_containers = 0;
   bool enabled = true;
-  int empty() const;
-  int used() const { return num_slots - empty(); }
+  int empty() const;  // free and enabled slots
+  int disabled() const;
+  int usable() const { return num_slots - disabled(); }
+  int used() const { return usable() - empty(); }
+  bool free_slot(int i) const { return slot_owner[i].empty() && !slot_disabled[i]; }
 };
 
 struct Request {
@@ -56,6 +60,9 @@ class Scheduler {
   void add_agent(const std::string& id, int slots);
   void remove_agent(const std::string& id);  // allocations on it become unallocated (returned lost)
   void set_agent_enabled(const std::string& id, bool enabled);
+  // Disable / enable one slot of an agent: a disabled slot is never offered to new allocations
+  // (a running allocation on it keeps it until it ends).  Returns false for an unknown slot.
+  bool set_slot_enabled(const std::string& id, int slot, bool enabled);
   void add_request(const Request& r);
   void remove_request(const std::string& alloc_id);  // frees its slots
   void set_priority(const std::string& job_id, int priority);

@@ -292,10 +292,12 @@ def agent_list(a):
 def slot_list(a):
     rows = []
     for ag in _session(a).get("/api/v1/agents")["agents"]:
+        disabled = set(ag.get("disabled_slots") or [])
         for i, owner in enumerate(ag["slot_owner"]):
             rows.append({"agent": ag["id"], "slot": i, "device": ag["devices"][i] if i < len(ag["devices"]) else i,
-                         "type": "rocm" if ag["gpu"] else "cpu", "allocation": owner or ""})
-    _print(rows, ["agent", "slot", "device", "type", "allocation"], a)
+                         "type": "rocm" if ag["gpu"] else "cpu", "enabled": i not in disabled and ag["enabled"],
+                         "allocation": owner or ""})
+    _print(rows, ["agent", "slot", "device", "type", "enabled", "allocation"], a)
 
 
 def pool_list(a):

@@ -50,6 +50,17 @@ def register(sub: argparse._SubParsersAction, session: Callable, show: Callable,
     _add(ag, "enable", agent_toggle(True), "agent_id")
     _add(ag, "disable", agent_toggle(False), "agent_id")
 
+    def slot_toggle(enable: bool):  # reference cli/agent.py patch_slot
+        def fn(a):
+            verb = "enable" if enable else "disable"
+            session(a).post(f"/api/v1/agents/{a.agent_id}/slots/{a.slot_id}/{verb}", {})
+            print(f"{verb}d slot {a.slot_id} of agent {a.agent_id}")
+        return fn
+
+    sl = _group(sub, "slot")
+    _add(sl, "enable", slot_toggle(True), "agent_id", (("slot_id",), {"type": int}))
+    _add(sl, "disable", slot_toggle(False), "agent_id", (("slot_id",), {"type": int}))
+
     # ---------------------------------------------------------------- checkpoint rm / experiment aliases
     ck = _group(sub, "checkpoint")
     _add(ck, "rm", ck.choices["delete"]._defaults["fn"], (("uuids",), {"nargs": "+"}))

@@ -19,6 +19,7 @@ master-proxied download in this build.
 """
 
 import base64
+import contextvars
 import enum
 import io
 import json
@@ -33,6 +34,8 @@ import yaml
 from determined_amd.common.api import NotFoundException, Session
 
 _session: Optional[Session] = None
+# set by ``Determined`` objects (experimental/determined.py) while one of their methods runs
+_override: "contextvars.ContextVar[Optional[Session]]" = contextvars.ContextVar("damd_sdk_session", default=None)
 
 
 def login(master: Optional[str] = None, user: Optional[str] = None, password: Optional[str] = None,
@@ -54,6 +57,9 @@ def logout() -> None:
 
 
 def _s() -> Session:
+    bound = _override.get()
+    if bound is not None:
+        return bound
     if _session is None:
         login()
     assert _session is not None
@@ -272,11 +278,11 @@ class Trial:
             return max(cks, key=lambda c: c.steps_completed or 0)
         return self.top_checkpoint(sort_by, smaller_is_better)
 
-    def iter_metrics(self, group: str) -> Iterator[Dict[str, Any]]:
+    def iter_metrics(self, group: str) -> Iterator["TrialMetrics"]:
+        """``TrialMetrics`` reports of one group (``TrainingMetrics`` / ``ValidationMetrics``)."""
         rows = self._session.get(f"/api/v1/trials/{self.id}/metrics", params={"group": group})["metrics"]
         for r in rows:
-            yield {"trial_id": self.id, "steps_completed": r["steps_completed"], "metrics": r["metrics"],
-                   "group": r["group_name"], "trial_run_id": r.get("trial_run_id"), "time": r.get("ts")}
+            yield TrialMetrics._from_row(self.id, r)
 
     def stream_training_metrics(self) -> Iterable[Dict[str, Any]]:
         return self.iter_metrics("training")
@@ -825,9 +831,10 @@ class Workspace:
     def delete_project(self, name: str) -> None:
         self._session.delete(f"/api/v1/projects/{self.get_project(name).id}")
 
-    def list_pools(self) -> List[Dict[str, Any]]:
-        """Resource pools usable from this workspace (every pool: pools are not bound to workspaces)."""
-        return list(self._session.get("/api/v1/resource-pools").get("resource_pools") or [])
+    def list_pools(self) -> List["ResourcePool"]:
+        """Resource pools usable from this workspace (unbound pools + pools bound to it)."""
+        rows = self._session.get(f"/api/v1/workspaces/{self.id}/available-resource-pools").get("resource_pools") or []
+        return [ResourcePool(self._session, r["name"] if isinstance(r, dict) else str(r)) for r in rows]
 
     def __repr__(self) -> str:
         return f"Workspace(id={self.id}, name={self.name})"
@@ -855,3 +862,22 @@ def get_model_by_id(model_id: int) -> Model:
 
 def stream_trials_metrics(trial_ids: List[int], group: str) -> Iterable[Dict[str, Any]]:
     return iter_trials_metrics(trial_ids, group)
+
+
+def list_resource_pools() -> List["ResourcePool"]:
+    return _list_resource_pools(_s())
+
+
+def get_resource_pool(name: str) -> "ResourcePool":
+    return ResourcePool(_s(), name)
+
+
+from determined_amd.experimental.determined import (  # noqa: E402  (cyclic: determined.py imports this lazily)
+    Determined,
+    ResourcePool,
+    TrainingMetrics,
+    TrialMetrics,
+    ValidationMetrics,
+    list_resource_pools as _list_resource_pools,
+    test_one_batch,
+)

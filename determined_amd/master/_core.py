@@ -801,7 +801,8 @@ class Master:
             self.agents[agent_id] = {"id": agent_id, "slots": slots, "host": host, "devices": devices or list(range(slots)),
                                      "gpu": gpu, "label": label, "queue": existing["queue"] if existing else [],
                                      "last_seen": time.time(), "enabled": existing["enabled"] if existing else True,
-                                     "resource_pool": pool}
+                                     "resource_pool": pool,
+                                     "disabled_slots": list((existing or {}).get("disabled_slots") or [])}
             if existing is None:
                 self.sched.add_agent(agent_id, slots, pool)
             self.cv.notify_all()

@@ -103,6 +103,10 @@ class PoolSet:
         if name is not None:
             self.pools[name].sched.set_agent_enabled(agent_id, enabled)
 
+    def set_slot_enabled(self, agent_id: str, slot: int, enabled: bool) -> bool:
+        name = self._agent_pool.get(agent_id)
+        return name is not None and bool(self.pools[name].sched.set_slot_enabled(agent_id, int(slot), enabled))
+
     # ---------------------------------------------------------------- requests
     def add_request(self, alloc_id: str, job_id: str, slots: int, priority: int = 42, weight: float = 1.0,
                     order: int = 0, preemptible: bool = True, excluded_agents: Optional[List[str]] = None,

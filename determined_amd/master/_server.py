@@ -431,8 +431,25 @@ def build_routes(m: Master) -> List[Route]:
             out.append({"id": aid, "host": ag["host"], "slots": ag["slots"], "devices": ag["devices"],
                         "gpu": ag["gpu"], "enabled": ag["enabled"], "label": ag["label"],
                         "resource_pool": ag.get("resource_pool", m.sched.default_compute),
-                        "slot_owner": owners, "used_slots": sum(1 for o in owners if o)})
+                        "slot_owner": owners, "used_slots": sum(1 for o in owners if o),
+                        "disabled_slots": list(sa.get(aid, {}).get("disabled_slots", []))})
         return {"agents": out}
+
+    @route("POST", r"/api/v1/agents/([^/]+)/slots/(\d+)/(enable|disable)")
+    def slot_enable(q, b, agent_id, slot, what):
+        """``det slot enable|disable`` (reference ``api_agents.go`` EnableSlot / DisableSlot): a
+        disabled slot gets no new allocations; one running on it keeps it until it ends."""
+        m.iam.require("admin_cluster")
+        with m.lock:
+            if agent_id not in m.agents:
+                raise HTTPError(404, f"agent {agent_id} not found")
+            if not m.sched.set_slot_enabled(agent_id, int(slot), what == "enable"):
+                raise HTTPError(404, f"slot {slot} of agent {agent_id} not found")
+            dis = set(m.agents[agent_id].get("disabled_slots") or [])
+            (dis.discard if what == "enable" else dis.add)(int(slot))
+            m.agents[agent_id]["disabled_slots"] = sorted(dis)
+            m._schedule()
+        return {"agent_id": agent_id, "slot_id": int(slot), "enabled": what == "enable"}
 
     @route("POST", r"/api/v1/agents/([^/]+)/(enable|disable)")
     def agent_enable(q, b, agent_id, what):

@@ -41,6 +41,15 @@ def test_cluster_and_admin_verbs(master, tmp_path):
     det(url, "agent", "disable", "n1")
     assert not s.get("/api/v1/agents")["agents"][0]["enabled"]
     det(url, "agent", "enable", "n1")
+    det(url, "slot", "disable", "n1", "1")
+    ag = s.get("/api/v1/agents")["agents"][0]
+    assert ag["disabled_slots"] == [1]
+    rows = json.loads(det(url, "--json", "slot", "list"))
+    assert [r["enabled"] for r in rows] == [True, False]
+    s.post("/api/v1/agents/register", {"agent_id": "n1", "slots": 2})  # re-registration keeps it
+    assert s.get("/api/v1/agents")["agents"][0]["disabled_slots"] == [1]
+    det(url, "slot", "enable", "n1", "1")
+    assert s.get("/api/v1/agents")["agents"][0]["disabled_slots"] == []
     assert "resource_pools" in det(url, "master", "config", "show")
     assert "log level: debug" in det(url, "master", "config", "set", "--log-level", "debug")
     det(url, "master", "config", "set", "--log-level", "info")

@@ -88,3 +88,53 @@ def test_single_default_pool_without_config():
     finally:
         srv.stop()
         srv.master.close()
+
+
+def test_sdk_resource_pool_and_determined_object(pooled):
+    """SDK ``ResourcePool`` bindings + the object-style ``Determined`` client (reference
+    ``common/experimental/{resource_pool,determined}.py``)."""
+    from determined_amd.experimental import Determined, ResourcePool, client
+
+    srv, s = pooled
+    d = Determined(f"http://127.0.0.1:{srv.port}")
+    assert sorted(p.name for p in d.list_resource_pools()) == ["aux", "train"]
+    w = d.create_workspace("vision")
+    w.create_project("detection")
+    rp = d.get_resource_pool("train")
+    assert isinstance(rp, ResourcePool) and rp.describe()["scheduler_type"] == "fair_share"
+    rp.add_bindings(["vision"])
+    assert rp.list_workspaces() == ["vision"]
+    assert sorted(p.name for p in w.list_pools()) == ["aux", "train"]
+    assert [p.name for p in d.get_workspace("Uncategorized").list_pools()] == ["aux"]
+    rp.replace_bindings([])
+    assert rp.list_workspaces() == []
+    rp.add_bindings(["vision"])
+    rp.remove_bindings(["vision"])
+    assert rp.list_workspaces() == []
+    exp = d.create_experiment(dict(CFG, workspace="vision", project="detection"), activate=False)
+    assert [e.id for e in d.list_experiments()] == [exp.id]
+    assert d.get_experiment(exp.id).config["resources"]["resource_pool"] == "train"
+    # the object's session never leaks into the module-level client
+    assert client._override.get() is None
+
+
+def test_test_one_batch_runs_a_trial_locally(tmp_path, monkeypatch):
+    """``experimental.test_one_batch`` (reference ``experimental/_native.py``): one training
+    batch + validation + checkpoint of a PyTorchTrial in test mode."""
+    import os
+    import sys
+
+    from determined_amd.experimental import test_one_batch
+
+    monkeypatch.chdir(tmp_path)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "fixtures", "tiny_trial"))
+    try:
+        from model_def import TinyTrial
+
+        calls = []
+        orig = TinyTrial.train_batch
+        monkeypatch.setattr(TinyTrial, "train_batch", lambda self, *a, **k: calls.append(1) or orig(self, *a, **k))
+        test_one_batch(TinyTrial, {"hyperparameters": {"global_batch_size": 8, "lr": 0.1}})
+        assert len(calls) == 1
+    finally:
+        sys.path.pop(0)

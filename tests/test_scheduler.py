@@ -96,3 +96,33 @@ def test_round_robin_fifo_blocks():
     s.add_request("y", "2", 4, order=1)
     s.add_request("z", "3", 1, order=2)
     assert s.schedule()["allocated"] == ["x"]  # y blocks z (FIFO)
+
+
+def test_disabled_slots_are_never_offered():
+    """``det slot disable`` (reference agentrm slot enable/disable): a disabled slot is skipped by
+    shared fits, removes the agent from whole-agent gang fits and from the pool's capacity; a
+    slot disabled under a running allocation stays with it until it ends."""
+    s = sched()
+    s.add_agent("n", 4)
+    assert s.set_slot_enabled("n", 1, False) and not s.set_slot_enabled("n", 9, False)
+    assert s.total_slots == 3 and s.agents()["n"]["disabled_slots"] == [1]
+    s.add_request("a", "e", 3, order=0)
+    assert s.schedule()["allocated"] == ["a"]
+    assert s.requests()["a"]["assignment"] == [("n", [0, 2, 3])]
+    s.add_request("b", "e2", 1, order=1)
+    assert s.schedule()["allocated"] == []  # the only free slot is disabled
+    s.set_slot_enabled("n", 1, True)
+    assert s.schedule()["allocated"] == ["b"]
+    s.set_slot_enabled("n", 1, False)  # disabled while "b" holds it
+    assert s.used_slots == 4
+    s.remove_request("b")
+    assert s.used_slots == 3 and s.total_slots == 3
+    # whole-agent (multi-agent) gang fits skip agents with a disabled slot
+    g = sched()
+    g.add_agent("n0", 2)
+    g.add_agent("n1", 2)
+    g.set_slot_enabled("n1", 0, False)
+    g.add_request("gang", "e", 4)
+    assert g.schedule()["allocated"] == []
+    g.set_slot_enabled("n1", 0, True)
+    assert g.schedule()["allocated"] == ["gang"]
