@@ -74,11 +74,17 @@ def harness_step(batch: int, variant: str, bucket_mb: float, device: torch.devic
         all ranks of a multi-GPU run time their candidates alike; gradients are dropped after."""
         import contextlib
 
+        import torch.distributed as dist
         import torch.nn.functional as F
+
+        from determined_amd.ops.conv import agree_across_ranks
 
         x, yl = pool[0]
         sync_off = ctx._ddp[0].no_sync() if ctx._ddp else contextlib.nullcontext()
-        with sync_off:
+        # multi-GPU: candidate timings averaged over the ranks (a gloo group), so every rank runs
+        # the same kernels and no rank is slowed by a noisy pick
+        group = dist.new_group(backend="gloo") if dist.is_initialized() and dist.get_world_size() > 1 else None
+        with sync_off, agree_across_ranks(group):
             F.cross_entropy(trial.model(trial._prep(x)).float(), yl).backward()
         for m in ctx.models:
             m.zero_grad(set_to_none=True)

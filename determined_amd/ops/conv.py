@@ -16,8 +16,9 @@ Anything else -- other shapes, fp32 inputs, modules with hooks or parametrizatio
 module's own convolution (MIOpen).
 """
 
+import contextlib
 import os
-from typing import Callable, Dict, Optional, Tuple
+from typing import Callable, Dict, Iterator, List, Optional, Tuple
 
 import torch
 from torch import nn
@@ -196,9 +197,47 @@ def _prologue_pays(key: tuple, t_fused: Callable[[], float], t_plain: Callable[[
         return True  # A/B switch: the round-2 behaviour (1x1 prologues never timed)
     got = _TUNE.get(key)
     if got is None:
-        got = bool(_TUNE_ON and not torch.cuda.is_current_stream_capturing() and t_fused() < t_plain())
+        got = False
+        if _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+            tf, tp = _agreed([t_fused(), t_plain()])
+            got = tf < tp
         _TUNE[key] = got
     return bool(got)
+
+
+# Multi-rank runs: while set (``agree_across_ranks``), every candidate timing is replaced by its
+# mean over the ranks before the choice, so all ranks pick the same kernels (a data-parallel step
+# runs at the pace of the slowest rank; independent noisy picks would make some rank slower).
+_AGREE: Optional[Callable[[List[float]], List[float]]] = None
+
+
+def _agreed(times: List[float]) -> List[float]:
+    return list(_AGREE(times)) if _AGREE is not None else times
+
+
+@contextlib.contextmanager
+def agree_across_ranks(group=None) -> Iterator[None]:
+    """Inside this context the per-layer kernel timings are averaged over the ranks of ``group``
+    (a CPU/gloo process group; every rank must run the same layers in the same order, e.g. one
+    identical forward/backward per rank).  No-op without an initialised multi-rank group."""
+    global _AGREE
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        yield
+        return
+    world = dist.get_world_size(group)
+
+    def mean(v: List[float]) -> List[float]:
+        t = torch.tensor(v, dtype=torch.float64)
+        dist.all_reduce(t, group=group)
+        return (t / world).tolist()
+
+    prev, _AGREE = _AGREE, mean
+    try:
+        yield
+    finally:
+        _AGREE = prev
 
 
 def _time_once(fn: Callable[[], object], reps: int = 3, rounds: int = 2) -> float:
@@ -275,6 +314,7 @@ def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> obj
         choice = default if default in cands else next(iter(cands))
     else:
         times = {c: _time_once(fn) for c, fn in cands.items()}
+        times = dict(zip(times, _agreed(list(times.values()))))
         choice = min(times, key=times.get)
         if any(isinstance(c, int) and ops.ext().conv_sk_cfg(c) for c in cands):
             ops.conv_health_check()  # every candidate ran several times: a hand-off time-out shows here

@@ -144,3 +144,27 @@ def test_ddp_tail_bucket_is_small():
     m2(x).square().sum().backward()
     for p, q in zip(m.parameters(), m2.parameters()):
         torch.testing.assert_close(p.grad, q.grad)
+
+
+def _agree_worker(rank, world):
+    import torch
+
+    from determined_amd.ops import conv
+
+    torch.cuda.is_current_stream_capturing = lambda: False  # CPU-only process
+    conv._TUNE_ON = True
+    # rank 0 alone would fuse (1 < 2); the mean over the ranks (3 vs 2) says no -- on every rank
+    t_f = {0: 1.0, 1: 5.0}[rank]
+    with conv.agree_across_ranks():
+        got = conv._prologue_pays(("agree_test",), lambda: t_f, lambda: 2.0)
+        mean = conv._agreed([float(rank), 10.0])
+    outside = conv._agreed([float(rank)])
+    return torch.tensor([float(got), mean[0], mean[1], outside[0]])
+
+
+def test_conv_tuning_agrees_across_ranks():
+    """Multi-GPU bench tuning (ops/conv.py agree_across_ranks): candidate timings are averaged
+    over the ranks, so every rank makes the same kernel choice."""
+    outs = run_distributed(_agree_worker, world=2)
+    assert outs[0].tolist() == [0.0, 0.5, 10.0, 0.0]
+    assert outs[1].tolist() == [0.0, 0.5, 10.0, 1.0]
