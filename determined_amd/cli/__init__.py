@@ -37,8 +37,17 @@ def _print(rows: List[Dict[str, Any]], cols: List[str], a: argparse.Namespace) -
     print(tabulate([[r.get(c) for c in cols] for r in rows], headers=cols))
 
 
-def tar_model_dir(model_dir: str) -> bytes:
+def tar_model_dir(model_dir: str, includes: Optional[List[str]] = None) -> bytes:
+    """gzip tar of the model definition (a directory or a single file) plus ``includes``
+    (``det e create -i``: extra files / directories, added under their base names)."""
     root = pathlib.Path(model_dir)
+    if root.is_file():
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w:gz") as tf:
+            tf.add(root, arcname=root.name)
+            for inc in includes or []:
+                tf.add(inc, arcname=pathlib.Path(inc).name)
+        return buf.getvalue()
     ignore = set()
     dignore = root / ".detignore"
     if dignore.exists():
@@ -50,6 +59,8 @@ def tar_model_dir(model_dir: str) -> bytes:
             if any(part in ("__pycache__", ".git") for part in rel.parts) or any(rel.match(g) for g in ignore):
                 continue
             tf.add(p, arcname=str(rel), recursive=False)
+        for inc in includes or []:
+            tf.add(inc, arcname=pathlib.Path(inc).name)
     data = buf.getvalue()
     if len(data) > 96 * 1024 * 1024:
         raise SystemExit("model definition directory is larger than 96 MiB; add a .detignore")
@@ -74,8 +85,13 @@ def exp_create(a: argparse.Namespace) -> None:
     if a.local:
         return _exp_local(cfg, a)
     s = _session(a)
-    body = {"config": cfg, "model_def": base64.b64encode(tar_model_dir(a.model_def)).decode(),
-            "activate": not a.paused}
+    body: Dict[str, Any] = {"config": cfg, "activate": not a.paused}
+    if a.model_def is not None:
+        body["model_def"] = base64.b64encode(tar_model_dir(a.model_def, a.include)).decode()
+    if a.template:
+        body["template"] = a.template
+    if a.project_id is not None:
+        body["project_id"] = a.project_id
     r = s.post("/api/v1/experiments", body)
     eid = r["experiment"]["id"]
     print(f"Created experiment {eid}")
@@ -99,7 +115,7 @@ def _exp_local(cfg: Dict[str, Any], a: argparse.Namespace) -> None:
     env = dict(os.environ)
     env.update(DET_LOCAL_HPARAMS=json.dumps(hp), DET_LOCAL_CONFIG=json.dumps(cfg))
     ep = cfg.get("entrypoint")
-    code = subprocess.call([sys.executable, "-m", "determined_amd.exec.local", ep], cwd=a.model_def, env=env)
+    code = subprocess.call([sys.executable, "-m", "determined_amd.exec.local", ep], cwd=a.model_def or ".", env=env)
     raise SystemExit(code)
 
 
@@ -314,7 +330,8 @@ def cmd_run(a):
     s = _session(a)
     r = s.post("/api/v1/commands", {"command": " ".join(a.cmd), "slots": a.slots,
                                     "resource_pool": getattr(a, "resource_pool", None),
-                                    "priority": getattr(a, "priority", None)})
+                                    "priority": getattr(a, "priority", None),
+                                    "template": getattr(a, "template", None)})
     print(f"Launched command {r['task_id']}")
     if not a.detach:
         _follow_logs(s, r["task_id"], lambda: s.get(f"/api/v1/tasks/{r['task_id']}")["task"]["state"] in
@@ -411,10 +428,13 @@ def build_parser() -> argparse.ArgumentParser:
     e = sub.add_parser("experiment", aliases=["e"]).add_subparsers(dest="verb", required=True)
     c = e.add_parser("create")
     c.add_argument("config_file")
-    c.add_argument("model_def")
+    c.add_argument("model_def", nargs="?", default=None)
+    c.add_argument("-i", "--include", action="append", default=[], help="extra files to ship with the model")
+    c.add_argument("--template", default=None, help="template to apply to the experiment config")
+    c.add_argument("--project_id", "--project-id", type=int, default=None, dest="project_id")
     c.add_argument("--paused", action="store_true")
     c.add_argument("-f", "--follow-first-trial", action="store_true")
-    c.add_argument("--test", "--test-mode", action="store_true", dest="test")
+    c.add_argument("-t", "--test", "--test-mode", action="store_true", dest="test")
     c.add_argument("--local", action="store_true")
     c.add_argument("--config", action="append", help="override: key.sub=value")
     c.set_defaults(fn=exp_create)
@@ -508,7 +528,8 @@ def build_parser() -> argparse.ArgumentParser:
     ck_.set_defaults(fn=lambda a: _session(a).post(f"/api/v1/tasks/{a.task_id}/kill", {}))
     cr = cm.add_parser("run")
     cr.add_argument("cmd", nargs=argparse.REMAINDER)
-    cr.add_argument("--slots", type=int, default=0)
+    cr.add_argument("--slots", type=int, default=None)
+    cr.add_argument("--template", default=None, help="template to apply to the command config")
     cr.add_argument("-d", "--detach", action="store_true")
     cr.set_defaults(fn=cmd_run)
 

@@ -57,6 +57,27 @@ def _guard_exp(m: Master, eid: Any, perm: str) -> Dict[str, Any]:
     return row
 
 
+def deep_merge(primary: Any, fallback: Any) -> Any:
+    """``primary`` with the keys it lacks filled from ``fallback``, recursively through dicts
+    (reference ``schemas.Merge``: the experiment's own settings win over the template's)."""
+    if isinstance(primary, dict) and isinstance(fallback, dict):
+        out = dict(fallback)
+        for k, v in primary.items():
+            out[k] = deep_merge(v, fallback[k]) if k in fallback else v
+        return out
+    return primary
+
+
+def merge_template(m: Master, cfg: Dict[str, Any], name: str) -> Dict[str, Any]:
+    row = m.db.one("SELECT * FROM templates WHERE name=?", [name])
+    if row is None:
+        raise HTTPError(404, f"template {name} not found")
+    tcfg = row["config"]
+    if isinstance(tcfg, (str, bytes)):
+        tcfg = json.loads(tcfg)
+    return deep_merge(cfg, tcfg or {})
+
+
 def _exp_summary(m: Master, row: Dict[str, Any]) -> Dict[str, Any]:
     cfg = row.get("config") or {}
     n = m.db.one("SELECT COUNT(*) AS n FROM trials WHERE experiment_id=?", [row["id"]])
@@ -117,9 +138,18 @@ def build_routes(m: Master) -> List[Route]:
     def create_exp(q, b):
         md = base64.b64decode(b["model_def"]) if b.get("model_def") else None
         cfg0 = b["config"] if isinstance(b.get("config"), dict) else {}
+        if b.get("template"):  # reference core_experiment.go: schemas.Merge(config, template)
+            cfg0 = merge_template(m, cfg0, b["template"])
+        if b.get("project_id") is not None:  # place the experiment in this project
+            proj = m.db.one("SELECT * FROM projects WHERE id=?", [int(b["project_id"])])
+            if proj is None:
+                raise HTTPError(404, f"project {b['project_id']} not found")
+            ws = m.db.one("SELECT name FROM workspaces WHERE id=?", [proj["workspace_id"]])
+            cfg0 = dict(cfg0, workspace=ws["name"], project=proj["name"])
         m.iam.resolve_target(cfg0)
         try:
-            eid = m.create_experiment(b["config"], md, activate=b.get("activate", True),
+            eid = m.create_experiment(cfg0 if isinstance(b.get("config"), dict) else b["config"], md,
+                                      activate=b.get("activate", True),
                                       parent_id=b.get("parent_id"), unmanaged=bool(b.get("unmanaged")))
         except InvalidConfig as e:
             raise HTTPError(400, str(e))
@@ -374,7 +404,23 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("POST", "/api/v1/commands")
     def create_cmd(q, b):
-        tid = m.create_command(b["command"], int(b.get("slots", 0)), b.get("env"), b.get("type", "COMMAND"),
+        if b.get("template"):  # reference api_command.go: the template's config fills what the request lacks
+            tcfg = merge_template(m, {}, b["template"])
+            res = tcfg.get("resources") or {}
+            b = dict(b)
+            if b.get("slots") is None:
+                b["slots"] = res.get("slots", 0)
+            if b.get("resource_pool") is None:
+                b["resource_pool"] = res.get("resource_pool")
+            if b.get("priority") is None:
+                b["priority"] = res.get("priority")
+            env_vars = (tcfg.get("environment") or {}).get("environment_variables") or []
+            if isinstance(env_vars, dict):
+                env_vars = [f"{k}={v}" for k, v in env_vars.items()]
+            env = dict(kv.split("=", 1) for kv in env_vars if "=" in kv)
+            env.update(b.get("env") or {})
+            b["env"] = env or None
+        tid = m.create_command(b["command"], int(b.get("slots") or 0), b.get("env"), b.get("type", "COMMAND"),
                                b.get("workdir_b64"), b.get("resource_pool"), b.get("priority"))
         return {"task_id": tid}
 

@@ -163,3 +163,49 @@ def test_preview_search(tmp_path):
         main(["preview-search", str(f)])
     text = out.getvalue()
     assert "adaptive_asha" in text and "16 trial(s)" in text and "batches" in text
+
+
+def test_experiment_create_template_project_and_includes(master, tmp_path):
+    """``det e create --template/--project_id/-i`` (reference cli/experiment.py + core_experiment.go
+    ``schemas.Merge(config, template)``: the experiment's own settings win) and ``det cmd run
+    --template``."""
+    import base64
+    import io
+    import tarfile
+
+    srv, url = master
+    s = Session(url)
+    tpl = tmp_path / "tpl.yaml"
+    tpl.write_text(yaml.safe_dump({"max_restarts": 7, "resources": {"slots_per_trial": 2, "priority": 11},
+                                   "environment": {"environment_variables": ["FROM_TPL=1"]}}))
+    det(url, "template", "create", "team", str(tpl))
+    cfg = tmp_path / "exp.yaml"
+    cfg.write_text(yaml.safe_dump({"name": "tpl", "entrypoint": "model_def:T", "hyperparameters": {},
+                                   "resources": {"slots_per_trial": 1},
+                                   "searcher": {"name": "single", "metric": "loss", "max_length": {"batches": 1}}}))
+    model = tmp_path / "model"
+    model.mkdir()
+    (model / "model_def.py").write_text("T = None\n")
+    extra = tmp_path / "extra.txt"
+    extra.write_text("hello")
+    det(url, "workspace", "create", "ws")
+    det(url, "project", "create", "ws", "proj")
+    pid = next(p["id"] for p in s.get("/api/v1/workspaces/ws/projects")["projects"] if p["name"] == "proj")
+    out = det(url, "experiment", "create", str(cfg), str(model), "--paused", "--template", "team",
+              "--project_id", str(pid), "-i", str(extra))
+    eid = int(out.split()[-1])
+    exp = srv.master.experiments[eid]
+    assert exp.config["max_restarts"] == 7  # from the template
+    assert exp.config["resources"]["slots_per_trial"] == 1  # the experiment's own value wins
+    assert exp.config["resources"]["priority"] == 11
+    row = s.get(f"/api/v1/experiments/{eid}")["experiment"]
+    assert (row.get("workspace"), row.get("project")) == ("ws", "proj")
+    md = srv.master.db.one("SELECT model_def FROM experiments WHERE id=?", [eid])["model_def"]
+    names = tarfile.open(fileobj=io.BytesIO(md if isinstance(md, bytes) else base64.b64decode(md))).getnames()
+    assert {"model_def.py", "extra.txt"} <= set(names)
+    with pytest.raises(AssertionError):  # the CLI exits non-zero: template not found
+        det(url, "experiment", "create", str(cfg), str(model), "--paused", "--template", "nope")
+    # commands: slots / priority / env from the template
+    det(url, "cmd", "run", "-d", "--template", "team", "true")
+    job = [j for j in s.get("/api/v1/job-queues")["jobs"] if j["job_id"].startswith("command-")][-1]
+    assert job["priority"] == 11
