@@ -139,6 +139,8 @@ def main() -> int:
         dt = float(t.item())
 
     damd_ops.conv_health_check()
+    if rank == 0:
+        print(f"[bench] peak GPU memory {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     loss = float(state["last_loss"]()) if "last_loss" in state else float("nan")
     if rank == 0 and os.environ.get("DAMD_TUNE_DUMP"):  # per-layer kernel choices (A/B analysis)
         from determined_amd.ops.conv import tuned_choices
