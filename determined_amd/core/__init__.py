@@ -18,4 +18,5 @@ from determined_amd.core._searcher import (
 )
 from determined_amd.core._preempt import DummyPreemptContext, PreemptContext, PreemptMode
 from determined_amd.core._profiler import DummyProfilerContext, ProfilerContext
+from determined_amd.core._experimental import DummyExperimentalCoreContext, ExperimentalCoreContext
 from determined_amd.core._context import Context, InvalidHP, init, _dummy_init

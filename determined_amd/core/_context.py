@@ -14,6 +14,7 @@ from determined_amd import storage
 from determined_amd._info import get_cluster_info
 from determined_amd.core._checkpoint import CheckpointContext, DummyCheckpointContext
 from determined_amd.core._distributed import DistributedContext, DummyDistributedContext
+from determined_amd.core._experimental import DummyExperimentalCoreContext, ExperimentalCoreContext
 from determined_amd.core._preempt import DummyPreemptContext, PreemptContext, PreemptMode
 from determined_amd.core._profiler import DummyProfilerContext, ProfilerContext
 from determined_amd.core._searcher import DummySearcherContext, SearcherContext, _parse_searcher_units
@@ -31,7 +32,7 @@ class Context:
                  preempt: Optional[PreemptContext] = None, train: Optional[TrainContext] = None,
                  searcher: Optional[SearcherContext] = None, info: Any = None,
                  profiler: Optional[ProfilerContext] = None, _log_shipper: Any = None,
-                 _tensorboard_manager: Any = None) -> None:
+                 _tensorboard_manager: Any = None, experimental: Optional[ExperimentalCoreContext] = None) -> None:
         self.checkpoint = checkpoint
         self.distributed = distributed or DummyDistributedContext()
         self.preempt = preempt or DummyPreemptContext(self.distributed)
@@ -39,6 +40,7 @@ class Context:
         self.searcher = searcher or DummySearcherContext(self.distributed)
         self.info = info
         self.profiler = profiler or DummyProfilerContext()
+        self.experimental = experimental or DummyExperimentalCoreContext()
         self._log_shipper = _log_shipper
         self._tensorboard_manager = _tensorboard_manager
 
@@ -155,7 +157,8 @@ def init(*, distributed: Optional[DistributedContext] = None,
             _install_stacktrace_on_sigusr1()
             return Context(checkpoint=checkpoint, distributed=distributed,
                            preempt=DummyPreemptContext(distributed, preempt_mode), train=train,
-                           searcher=DummySearcherContext(distributed, 10**9), info=info, _tensorboard_manager=tb)
+                           searcher=DummySearcherContext(distributed, 10**9), info=info, _tensorboard_manager=tb,
+                           experimental=ExperimentalCoreContext(session, info.trial.trial_id))
         searcher = SearcherContext(session, distributed, info.trial.trial_id, info.trial._trial_run_id,
                                    info.allocation_id, _parse_searcher_units(cfg))
         checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,
@@ -166,7 +169,8 @@ def init(*, distributed: Optional[DistributedContext] = None,
         _install_stacktrace_on_sigusr1()
         return Context(checkpoint=checkpoint, distributed=distributed, preempt=preempt, train=train,
                        searcher=searcher, info=info, profiler=profiler,
-                       _log_shipper=maybe_log_shipper(session, info, distributed), _tensorboard_manager=tb)
+                       _log_shipper=maybe_log_shipper(session, info, distributed), _tensorboard_manager=tb,
+                       experimental=ExperimentalCoreContext(session, info.trial.trial_id))
     sm = sm or _default_local_storage()
     _install_stacktrace_on_sigusr1()
     return Context(checkpoint=DummyCheckpointContext(distributed, sm), distributed=distributed,

@@ -71,7 +71,19 @@ class DistributedContext:
         return cls(rank=rank, size=size, local_rank=local_rank, local_size=local_size, cross_rank=cross_rank,
                    cross_size=cross_size, chief_ip=chief_ip or os.environ.get("DET_CHIEF_IP"))
 
-    from_deepspeed = from_torch_distributed
+    @classmethod
+    def from_deepspeed(cls, chief_ip: Optional[str] = None) -> "DistributedContext":
+        """Build from the deepspeed launcher's env (RANK, WORLD_SIZE, LOCAL_RANK, LOCAL_SIZE,
+        CROSS_RANK, CROSS_SIZE; reference ``_distributed.py:from_deepspeed``), falling back to the
+        torchrun names where a variable is missing."""
+        if "LOCAL_SIZE" not in os.environ and "CROSS_SIZE" not in os.environ:
+            return cls.from_torch_distributed(chief_ip)
+        size = int(os.environ["WORLD_SIZE"])
+        local_size = int(os.environ.get("LOCAL_SIZE", os.environ.get("LOCAL_WORLD_SIZE", str(size))))
+        return cls(rank=int(os.environ["RANK"]), size=size, local_rank=int(os.environ["LOCAL_RANK"]),
+                   local_size=local_size, cross_rank=int(os.environ.get("CROSS_RANK", "0")),
+                   cross_size=int(os.environ.get("CROSS_SIZE", str(max(size // max(local_size, 1), 1)))),
+                   chief_ip=chief_ip or os.environ.get("DET_CHIEF_IP"))
 
     @classmethod
     def from_horovod(cls, hvd: Any = None, chief_ip: Optional[str] = None) -> "DistributedContext":

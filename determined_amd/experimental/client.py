@@ -185,12 +185,13 @@ class Checkpoint:
     def delete(self) -> None:
         self._session.delete(f"/api/v1/checkpoints/{self.uuid}")
 
-    def get_metrics(self, group: Optional[str] = None) -> Iterable[Dict[str, Any]]:
-        if self.trial_id is None:
-            return []
-        steps = self.steps_completed
-        return [m for m in Trial(self._session, self.trial_id).iter_metrics(group or "validation")
-                if m["steps_completed"] == steps]
+    def get_metrics(self, group: Optional[str] = None) -> Iterator["TrialMetrics"]:
+        """Metrics of the tasks that reported using this checkpoint
+        (``core_context.experimental.report_task_using_checkpoint``; reference
+        ``checkpoint/_checkpoint.py:get_metrics``); every group when ``group`` is None / ""."""
+        params = {"group": group} if group else {}
+        for r in self._session.get(f"/api/v1/checkpoints/{self.uuid}/metrics", params=params)["metrics"]:
+            yield TrialMetrics._from_row(r["trial_id"], r)
 
     def __repr__(self) -> str:
         return f"Checkpoint(uuid={self.uuid})"
@@ -531,8 +532,17 @@ class ModelVersion:
     def delete(self) -> None:
         self._session.delete(self._path())
 
-    def get_metrics(self, group: Optional[str] = None) -> Iterable[Dict[str, Any]]:
-        return self.checkpoint.get_metrics(group)
+    def get_metrics(self, group: Optional[str] = None) -> Iterator["TrialMetrics"]:
+        """Metrics of the tasks that reported using this model version
+        (``core_context.experimental.report_task_using_model_version``)."""
+        params = {"group": group} if group else {}
+        for r in self._session.get(f"{self._path()}/metrics", params=params)["metrics"]:
+            yield TrialMetrics._from_row(r["trial_id"], r)
+
+    @property
+    def model_id(self) -> Optional[int]:
+        mid = self._data.get("model_id")
+        return int(mid) if mid is not None else None
 
     def __repr__(self) -> str:
         return f"ModelVersion({self.model_name}, v{self.model_version})"

@@ -48,6 +48,9 @@ CREATE TABLE IF NOT EXISTS allocation_history (
   alloc_id TEXT PRIMARY KEY, task_id TEXT, kind TEXT, experiment_id INTEGER, owner TEXT, resource_pool TEXT,
   slots INTEGER, start_time REAL, end_time REAL);
 CREATE TABLE IF NOT EXISTS pool_bindings (pool TEXT, workspace_id INTEGER, PRIMARY KEY (pool, workspace_id));
+CREATE TABLE IF NOT EXISTS trial_source_infos (
+  trial_id INTEGER, checkpoint_uuid TEXT, source_type TEXT, model_id INTEGER, model_version INTEGER,
+  PRIMARY KEY (trial_id, checkpoint_uuid, source_type));
 """
 
 MIGRATIONS = [("experiments", "external_id", "TEXT"), ("trials", "external_id", "TEXT"), ("tasks", "proxy", "TEXT"),

@@ -309,6 +309,50 @@ def build_routes(m: Master) -> List[Route]:
                         + ("AND group_name=? " if grp else "") + "ORDER BY id", [int(tid)] + ([grp] if grp else []))
         return {"metrics": rows}
 
+    # ---------------------------------------------------------------- trial source info (reference
+    # api_trials.go ReportTrialSourceInfo / GetTrialMetricsByCheckpoint / ...ByModelVersion): a task
+    # that runs a checkpoint (batch inference) links itself to it, and the checkpoint's / model
+    # version's metrics are the metrics those tasks reported.
+    @route("POST", "/api/v1/trial-source-info")
+    def report_source_info(q, b):
+        info = b.get("trial_source_info") or b
+        tid = int(info["trial_id"])
+        if m.db.one("SELECT id FROM trials WHERE id=?", [tid]) is None:
+            raise HTTPError(404, f"trial {tid} not found")
+        uuid_ = info["checkpoint_uuid"]
+        if m.db.one("SELECT uuid FROM checkpoints WHERE uuid=?", [uuid_]) is None:
+            raise HTTPError(404, f"checkpoint {uuid_} not found")
+        m.db.execute("INSERT OR REPLACE INTO trial_source_infos (trial_id, checkpoint_uuid, source_type, model_id, "
+                     "model_version) VALUES (?,?,?,?,?)",
+                     [tid, uuid_, info.get("trial_source_info_type", "INFERENCE"), info.get("model_id"),
+                      info.get("model_version")])
+        return {"trial_id": tid, "checkpoint_uuid": uuid_}
+
+    def _source_metrics(where: str, args: List[Any], q: Dict[str, str]) -> Dict[str, Any]:
+        kind = q.get("trial_source_info_type", "INFERENCE")
+        grp = q.get("group") or q.get("metric_group")
+        tids = [int(r["trial_id"]) for r in m.db.all(
+            f"SELECT DISTINCT trial_id FROM trial_source_infos WHERE {where} AND source_type=? ORDER BY trial_id",
+            args + [kind])]
+        out = []
+        for tid in tids:
+            rows = m.db.all("SELECT group_name, steps_completed, metrics, trial_run_id, ts FROM metrics WHERE "
+                            "trial_id=? " + ("AND group_name=? " if grp else "") + "ORDER BY id",
+                            [tid] + ([grp] if grp else []))
+            out.extend(dict(r, trial_id=tid) for r in rows)
+        return {"metrics": out}
+
+    @route("GET", r"/api/v1/checkpoints/([^/]+)/metrics")
+    def checkpoint_metrics(q, b, uuid_):
+        return _source_metrics("checkpoint_uuid=?", [uuid_], q)
+
+    @route("GET", r"/api/v1/models/([^/]+)/versions/(\d+)/metrics")
+    def model_version_metrics(q, b, name, ver):
+        mod = m.db.one("SELECT id FROM models WHERE name=? OR CAST(id AS TEXT)=?", [name, name])
+        if mod is None:
+            raise HTTPError(404, f"model {name} not found")
+        return _source_metrics("model_id=? AND model_version=?", [int(mod["id"]), int(ver)], q)
+
     @route("POST", r"/api/v1/trials/(\d+)/early_exit")
     def trial_early_exit(q, b, tid):
         try:

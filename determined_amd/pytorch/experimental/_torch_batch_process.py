@@ -85,10 +85,14 @@ class TorchBatchProcessorContext(_PyTorchReducerContext):
         self._core_context.train.report_metrics(group=group, steps_completed=steps_completed, metrics=metrics)
 
     def report_task_using_checkpoint(self, checkpoint: Any) -> None:
-        logger.info("task uses checkpoint %s", getattr(checkpoint, "uuid", checkpoint))
+        """Link this task to ``checkpoint``: the metrics it reports become the checkpoint's
+        ``get_metrics()`` (core_context.experimental; chief only, like the reference)."""
+        if self._distributed.get_rank() == 0:
+            self._core_context.experimental.report_task_using_checkpoint(checkpoint)
 
     def report_task_using_model_version(self, model_version: Any) -> None:
-        logger.info("task uses model version %s", model_version)
+        if self._distributed.get_rank() == 0:
+            self._core_context.experimental.report_task_using_model_version(model_version)
 
     def get_distributed_rank(self) -> int:
         return self._distributed.get_rank()

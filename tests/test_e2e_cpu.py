@@ -304,3 +304,48 @@ def test_scheduler_excluded_agents():
     assert [ag for ag, _ in s.requests()["r1"]["assignment"]] == ["b"]
     s.add_request("r2", "j2", 2, excluded_agents=["a"])
     assert s.schedule()["allocated"] == []  # only "a" is free and it is excluded
+
+
+def test_trial_source_info_links_inference_metrics():
+    """``core_context.experimental.report_task_using_checkpoint / _model_version`` (reference
+    core/_experimental.py + api_trials.go ReportTrialSourceInfo): metrics an inference task
+    reports become the checkpoint's / model version's ``get_metrics()``."""
+    import uuid as _uuid
+
+    from determined_amd.common.api import Session
+    from determined_amd.core import ExperimentalCoreContext
+    from determined_amd.experimental import client
+    from determined_amd.master import start_master
+
+    srv = start_master()
+    try:
+        url = f"http://127.0.0.1:{srv.port}"
+        s = Session(url)
+        cfg = {"name": "src", "hyperparameters": {}, "searcher": {"name": "single", "metric": "loss",
+                                                                 "max_length": {"batches": 1}}}
+        eid = s.post("/api/v1/unmanaged/experiments", {"config": cfg})["experiment"]["id"]
+        train_tid = s.post(f"/api/v1/unmanaged/experiments/{eid}/trials", {"hparams": {}})["trial_id"]
+        infer_tid = s.post(f"/api/v1/unmanaged/experiments/{eid}/trials", {"hparams": {}})["trial_id"]
+        ck = str(_uuid.uuid4())
+        s.post("/api/v1/checkpoints", {"uuid": ck, "trial_id": train_tid, "steps_completed": 1,
+                                       "resources": {}, "metadata": {}})
+        s.post(f"/api/v1/trials/{train_tid}/metrics", {"group": "validation", "steps_completed": 1,
+                                                       "metrics": {"loss": 9.0}})
+        s.post(f"/api/v1/trials/{infer_tid}/metrics", {"group": "inference", "steps_completed": 5,
+                                                       "metrics": {"accuracy": 0.75}})
+        client.login(url)
+        ckpt = client.get_checkpoint(ck)
+        assert list(ckpt.get_metrics()) == []  # nothing linked yet (training metrics are not "usage")
+        ExperimentalCoreContext(s, infer_tid).report_task_using_checkpoint(ckpt)
+        got = list(ckpt.get_metrics("inference"))
+        assert [(m.trial_id, m.metrics, m.group) for m in got] == [(infer_tid, {"accuracy": 0.75}, "inference")]
+        assert list(ckpt.get_metrics("validation")) == []
+        model = client.create_model("src-model")
+        mv = model.register_version(ck)
+        assert list(mv.get_metrics()) == []
+        ExperimentalCoreContext(s, infer_tid).report_task_using_model_version(mv)
+        assert [m.metrics for m in mv.get_metrics("inference")] == [{"accuracy": 0.75}]
+    finally:
+        client.logout()
+        srv.stop()
+        srv.master.close()
