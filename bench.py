@@ -92,12 +92,9 @@ def main() -> int:
                                 use_harness=not a.no_harness)
 
     t_w = time.perf_counter()
-    if "tune" in state and not a.no_pretune:  # kernel choices outside the gradient all-reduce (all ranks alike)
-        state["tune"]()
-        if rank == 0:
-            print(f"[bench] conv kernels tuned ({time.perf_counter() - t_w:.1f}s)", file=sys.stderr, flush=True)
-    # the first warm-up step may spend minutes in MIOpen's solver search for shapes missing from
-    # the find-db: keep a heartbeat on stderr so supervisors do not mistake it for a hang
+    # kernel tuning and the first warm-up step may spend minutes in per-layer kernel timing and
+    # MIOpen's solver search for shapes missing from the find-db: keep a heartbeat on stderr from
+    # the start so supervisors do not mistake it for a hang
     import threading
 
     warm_done = threading.Event()
@@ -108,6 +105,10 @@ def main() -> int:
 
     if rank == 0:
         threading.Thread(target=heartbeat, daemon=True).start()
+    if "tune" in state and not a.no_pretune:  # kernel choices outside the gradient all-reduce (all ranks alike)
+        state["tune"]()
+        if rank == 0:
+            print(f"[bench] conv kernels tuned ({time.perf_counter() - t_w:.1f}s)", file=sys.stderr, flush=True)
     for i in range(a.warmup):
         step_fn()
         if rank == 0:  # progress on stderr (stdout carries only the JSON line)
