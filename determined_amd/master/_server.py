@@ -21,6 +21,7 @@ from determined_amd.master._iam import AuthError, _public_user
 from determined_amd.master._iam_routes import add_iam_routes
 from determined_amd.master._ntsc import add_ntsc_routes
 from determined_amd.master._exp_routes import add_exp_routes
+from determined_amd.master._runs_routes import add_runs_routes
 from determined_amd.master._webui import add_webui_routes
 from determined_amd.master._core import Master
 
@@ -477,6 +478,7 @@ def build_routes(m: Master) -> List[Route]:
 
     add_ntsc_routes(route, m)
     add_exp_routes(route, m)
+    add_runs_routes(route, m)
 
     @route("GET", "/api/v1/tasks")
     def list_tasks(q, b):
