@@ -297,6 +297,16 @@ def register(sub: argparse._SubParsersAction, session: Callable, show: Callable,
     _add(tp, "create", tpl_create, "name", "file")
     sv = tp.add_parser("set-value").add_subparsers(dest="field", required=True)
     _add(sv, "config", tpl_patch, "name", "file")
+    _add(tp, "config", tpl_patch, "name", "file")  # reference `det template config NAME FILE`
+
+    def task_pause(pause: bool):
+        def fn(a):
+            session(a).post(f"/api/v1/tasks/{a.task_id}/{'pause' if pause else 'unpause'}", {})
+            print(f"{'Paused' if pause else 'Unpaused'} task: {a.task_id}")
+        return fn
+
+    _add(tk, "pause", task_pause(True), "task_id")
+    _add(tk, "unpause", task_pause(False), "task_id")
 
     # ---------------------------------------------------------------- user extras
     def user_rename(a):
@@ -392,9 +402,23 @@ def register(sub: argparse._SubParsersAction, session: Callable, show: Callable,
         body = json.loads(a.data) if a.data else None
         print(json.dumps(s.request(a.x.upper(), a.path, body=body), indent=2, default=str))
 
+    def bindings_list(a):
+        for r in session(a).get("/api/v1/_routes")["routes"]:
+            print(f"{r['method']:6s} {r['path']}")
+
+    def bindings_call(a):  # reference cli/dev.py `det dev bindings call`: one REST route by method + path
+        s = session(a)
+        body = json.loads(a.body) if a.body else None
+        params = dict(kv.split("=", 1) for kv in a.param or [])
+        print(json.dumps(s.request(a.method.upper(), a.path, body=body, params=params or None), indent=2, default=str))
+
     dv = sub.add_parser("dev").add_subparsers(dest="verb", required=True)
     _add(dv, "auth-token", auth_token)
     _add(dv, "curl", curl, "path", (("-X",), {"dest": "x", "default": "GET"}), (("-d", "--data"), {"default": None}))
+    bd = dv.add_parser("bindings", aliases=["b"]).add_subparsers(dest="bverb", required=True)
+    _add(bd, "list", bindings_list)
+    _add(bd, "call", bindings_call, "method", "path", (("--body",), {"default": None}),
+         (("-p", "--param"), {"action": "append", "default": None}))
 
     # ---------------------------------------------------------------- preview-search
     def preview(a):

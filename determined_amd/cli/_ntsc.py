@@ -106,7 +106,14 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
         t = _wait_proxy(s, r["task_id"])
         print(f"Launched notebook {r['task_id']}: http://{t['proxy']['host']}:{t['proxy']['port']}/lab")
 
-    common(sub.add_parser("notebook"), "notebooks", nb_start, [(("--slots",), {"type": int, "default": 1})])
+    def nb_open(a):
+        t = session(a).get(f"/api/v1/tasks/{a.task_id}")["task"]
+        print(f"http://{t['proxy']['host']}:{t['proxy']['port']}/lab" if t.get("proxy") else "not ready")
+
+    nb = common(sub.add_parser("notebook"), "notebooks", nb_start, [(("--slots",), {"type": int, "default": 1})])
+    o = nb.add_parser("open")
+    o.add_argument("task_id")
+    o.set_defaults(fn=nb_open)
 
     # ---------------------------------------------------------------- shell
     def sh_start(a):

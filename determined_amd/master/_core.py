@@ -715,6 +715,46 @@ class Master:
         a.state = "TERMINATING"
         self.cv.notify_all()
 
+    def pause_task(self, task_id: str) -> None:
+        """``det task pause`` (reference ``api_generic_tasks.go`` PauseGenericTask): end the
+        task's allocation and park the task in PAUSED; ``unpause_task`` starts it again with the
+        same command, environment and resources."""
+        with self.lock:
+            row = self.db.one("SELECT * FROM tasks WHERE id=?", [task_id])
+            if row is None:
+                raise KeyError(f"task {task_id} not found")
+            if row["state"] in ("TERMINATED", "CANCELED", "PAUSED", "ERROR", "COMPLETED"):
+                raise ValueError(f"cannot pause task {task_id} in state {row['state']}")
+            live = [a for a in self.allocations.values() if a.task_id == task_id and a.state != "TERMINATED"]
+            for a in live:
+                a.pausing = True  # type: ignore[attr-defined]
+                self._kill_allocation(a)
+            if not live:
+                self.db.update("tasks", "id", task_id, state="PAUSED")
+            self.cv.notify_all()
+
+    def unpause_task(self, task_id: str) -> None:
+        with self.lock:
+            row = self.db.one("SELECT * FROM tasks WHERE id=?", [task_id])
+            if row is None:
+                raise KeyError(f"task {task_id} not found")
+            if row["state"] != "PAUSED":
+                raise ValueError(f"task {task_id} is not paused (state {row['state']})")
+            prev = [a for a in self.allocations.values() if a.task_id == task_id]
+            cfg = row.get("config") or {}
+            n = 1 + sum(1 for _ in prev)
+            aid = f"{task_id}.{n}"
+            a = Allocation(aid, task_id, int(cfg.get("slots", 0)), kind=row["type"])
+            last = prev[-1] if prev else None
+            a.command = cfg.get("cmd")  # type: ignore[attr-defined]
+            a.env = getattr(last, "env", {}) if last is not None else {}  # type: ignore[attr-defined]
+            a.workdir_b64 = getattr(last, "workdir_b64", None) if last is not None else None  # type: ignore[attr-defined]
+            self.allocations[aid] = a
+            self.db.update("tasks", "id", task_id, state="PENDING", end_time=None, exit_code=None)
+            self.sched.add_request(aid, task_id, a.slots, int(cfg.get("priority", 42)), float(cfg.get("weight", 1.0)),
+                                   self._next_order(), False, pool=cfg.get("resource_pool"))
+            self.cv.notify_all()
+
     def kill_task(self, task_id: str) -> None:
         with self.lock:
             for a in list(self.allocations.values()):
@@ -886,8 +926,10 @@ class Master:
         ok = all(c == 0 for c in a.exit_codes.values()) and bool(a.exit_codes)
         if a.kind != "TRIAL":
             code = max(a.exit_codes.values()) if a.exit_codes else -1
-            self.db.update("tasks", "id", a.task_id, state="TERMINATED" if not a.killed else "CANCELED",
-                           end_time=time.time(), exit_code=code)
+            state = "TERMINATED" if not a.killed else "CANCELED"
+            if getattr(a, "pausing", False):
+                state = "PAUSED"  # det task pause: the allocation ended, the task waits for unpause
+            self.db.update("tasks", "id", a.task_id, state=state, end_time=time.time(), exit_code=code)
             return
         exp = self.experiments.get(a.exp_id)  # type: ignore[arg-type]
         if exp is None:

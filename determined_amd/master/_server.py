@@ -469,6 +469,21 @@ def build_routes(m: Master) -> List[Route]:
                                b.get("workdir_b64"), b.get("resource_pool"), b.get("priority"))
         return {"task_id": tid}
 
+    @route("POST", r"/api/v1/tasks/([^/]+)/(pause|unpause)")
+    def task_pause(q, b, task_id, what):
+        try:
+            (m.pause_task if what == "pause" else m.unpause_task)(task_id)
+        except KeyError as e:
+            raise HTTPError(404, str(e))
+        except ValueError as e:
+            raise HTTPError(400, str(e))
+        return {}
+
+    @route("GET", "/api/v1/_routes")
+    def list_routes(q, b):
+        """Every REST route of this master (``det dev bindings list``)."""
+        return {"routes": [{"method": meth, "path": rx.pattern.strip("^$")} for meth, rx, _ in routes]}
+
     @route("POST", r"/api/v1/tasks/([^/]+)/proxy")
     def task_proxy(q, b, task_id):
         if m.db.one("SELECT id FROM tasks WHERE id=?", [task_id]) is None:

@@ -209,3 +209,38 @@ def test_experiment_create_template_project_and_includes(master, tmp_path):
     det(url, "cmd", "run", "-d", "--template", "team", "true")
     job = [j for j in s.get("/api/v1/job-queues")["jobs"] if j["job_id"].startswith("command-")][-1]
     assert job["priority"] == 11
+
+
+def test_task_pause_unpause_dev_bindings_template_config(master, tmp_path):
+    """``det task pause/unpause`` (reference api_generic_tasks.go: the allocation ends, the task
+    waits in PAUSED, unpause starts it again), ``det dev bindings list/call``, ``det template
+    config`` and ``det notebook open``."""
+    srv, url = master
+    s = Session(url)
+    s.post("/api/v1/agents/register", {"agent_id": "n1", "slots": 2})
+    tid = s.post("/api/v1/commands", {"command": ["sleep", "30"], "slots": 1, "type": "GENERIC"})["task_id"]
+    with srv.master.lock:
+        srv.master._schedule()
+    det(url, "task", "pause", tid)
+    alloc = next(a for a in srv.master.allocations.values() if a.task_id == tid)
+    with srv.master.lock:  # the agent reports the killed process
+        alloc.exit_codes = {0: -15}
+        srv.master._finish_allocation(alloc)
+    assert s.get(f"/api/v1/tasks/{tid}")["task"]["state"] == "PAUSED"
+    with pytest.raises(AssertionError):
+        det(url, "task", "pause", tid)  # already paused
+    det(url, "task", "unpause", tid)
+    assert s.get(f"/api/v1/tasks/{tid}")["task"]["state"] in ("PENDING", "RUNNING")
+    allocs = [a for a in srv.master.allocations.values() if a.task_id == tid]
+    assert len(allocs) == 2 and allocs[-1].command == ["sleep", "30"]
+    det(url, "cmd", "kill", tid)
+    out = det(url, "dev", "bindings", "list")
+    assert "POST   /api/v1/tasks/([^/]+)/(pause|unpause)" in out and "GET    /api/v1/agents" in out
+    assert json.loads(det(url, "dev", "bindings", "call", "GET", "/api/v1/agents"))["agents"][0]["id"] == "n1"
+    f = tmp_path / "t.yaml"
+    f.write_text(yaml.safe_dump({"resources": {"slots_per_trial": 2}}))
+    det(url, "template", "create", "tc", str(f))
+    f.write_text(yaml.safe_dump({"max_restarts": 3}))
+    det(url, "template", "config", "tc", str(f))
+    assert s.get("/api/v1/templates/tc")["template"]["config"] == {"resources": {"slots_per_trial": 2}, "max_restarts": 3}
+    assert det(url, "notebook", "open", tid).strip() == "not ready"
