@@ -372,18 +372,50 @@ def _local_dir() -> pathlib.Path:
     return d
 
 
-def cluster_up(a):
+def _pids() -> Dict[str, int]:
+    f = _local_dir() / "pids.json"
+    return json.loads(f.read_text()) if f.exists() else {}
+
+
+def _save_pids(pids: Dict[str, int]) -> None:
+    f = _local_dir() / "pids.json"
+    if pids:
+        f.write_text(json.dumps(pids))
+    elif f.exists():
+        f.unlink()
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+        return True
+    except (ProcessLookupError, PermissionError):
+        return False
+
+
+def _stop(pids: Dict[str, int], name: str) -> None:
+    pid = pids.pop(name, None)
+    if pid is None:
+        return
+    try:
+        os.killpg(pid, signal.SIGTERM)
+    except ProcessLookupError:
+        pass
+
+
+def _start_master(a, pids: Dict[str, int]) -> str:
+    """``det deploy local master-up`` (reference deploy/local/cli.py): the master as a local process
+    (sqlite db + logs under the local cluster directory)."""
     d = _local_dir()
-    pids: Dict[str, int] = {}
-    pidfile = d / "pids.json"
-    if pidfile.exists():
-        raise SystemExit(f"a local cluster seems to be running ({pidfile}); run `det deploy local cluster-down`")
+    if "master" in pids and _alive(pids["master"]):
+        raise SystemExit(f"a local master is already running (pid {pids['master']}); run `det deploy local master-down`")
     port = a.master_port
-    env = dict(os.environ)
+    cmd = [sys.executable, "-m", "determined_amd.master", "--port", str(port), "--db", str(d / "master.db"),
+           "--scheduler", a.scheduler]
+    if getattr(a, "master_config_path", None):
+        cmd += ["--config-file", str(a.master_config_path)]
     mlog = open(d / "master.log", "a")
-    mp = subprocess.Popen([sys.executable, "-m", "determined_amd.master", "--port", str(port), "--db",
-                           str(d / "master.db"), "--scheduler", a.scheduler], stdout=mlog, stderr=subprocess.STDOUT,
-                          env=env, start_new_session=True)
+    mp = subprocess.Popen(cmd, stdout=mlog, stderr=subprocess.STDOUT, env=dict(os.environ), start_new_session=True)
     pids["master"] = mp.pid
     url = f"http://127.0.0.1:{port}"
     s = Session(url, max_retries=0)
@@ -392,30 +424,101 @@ def cluster_up(a):
             s.get("/api/v1/master")
             break
         except Exception:
+            if mp.poll() is not None:
+                raise SystemExit(f"the master exited (code {mp.returncode}); see {d / 'master.log'}")
             time.sleep(0.2)
+    return url
+
+
+def _start_agent(name: str, url: str, a, pids: Dict[str, int]) -> None:
+    d = _local_dir()
+    key = f"agent-{name}" if not name.startswith("agent-") else name
+    if key in pids and _alive(pids[key]):
+        raise SystemExit(f"agent {key} is already running (pid {pids[key]})")
+    alog = open(d / f"{key}.log", "a")
+    cmd = [sys.executable, "-m", "determined_amd.agent", "--master-url", url, "--agent-id", key]
+    if a.no_gpu:
+        cmd += ["--slots", str(a.cpu_slots)]
+    if getattr(a, "resource_pool", None):
+        cmd += ["--resource-pool", a.resource_pool]
+    ap = subprocess.Popen(cmd, stdout=alog, stderr=subprocess.STDOUT, env=dict(os.environ), start_new_session=True)
+    pids[key] = ap.pid
+
+
+def cluster_up(a):
+    pids = _pids()
+    if any(_alive(p) for p in pids.values()):
+        raise SystemExit(f"a local cluster seems to be running ({_local_dir() / 'pids.json'}); "
+                         "run `det deploy local cluster-down`")
+    pids = {}
+    url = _start_master(a, pids)
     for i in range(a.agents):
-        alog = open(d / f"agent-{i}.log", "a")
-        cmd = [sys.executable, "-m", "determined_amd.agent", "--master-url", url, "--agent-id", f"agent-{i}"]
-        if a.no_gpu:
-            cmd += ["--slots", str(a.cpu_slots)]
-        ap = subprocess.Popen(cmd, stdout=alog, stderr=subprocess.STDOUT, env=env, start_new_session=True)
-        pids[f"agent-{i}"] = ap.pid
-    pidfile.write_text(json.dumps(pids))
-    print(f"local cluster up: master {url}, {a.agents} agent(s); logs in {d}")
+        _start_agent(str(i), url, a, pids)
+    _save_pids(pids)
+    print(f"local cluster up: master {url}, {a.agents} agent(s); logs in {_local_dir()}")
 
 
 def cluster_down(a):
-    pidfile = _local_dir() / "pids.json"
-    if not pidfile.exists():
+    pids = _pids()
+    if not pids:
         print("no local cluster running")
         return
-    for name, pid in json.loads(pidfile.read_text()).items():
-        try:
-            os.killpg(pid, signal.SIGTERM)
-        except ProcessLookupError:
-            pass
-    pidfile.unlink()
+    for name in list(pids):
+        _stop(pids, name)
+    _save_pids(pids)
     print("local cluster down")
+
+
+def master_up(a):
+    pids = _pids()
+    url = _start_master(a, pids)
+    _save_pids(pids)
+    print(f"local master up: {url}; logs in {_local_dir() / 'master.log'}")
+
+
+def master_down(a):
+    pids = _pids()
+    if "master" not in pids:
+        print("no local master running")
+        return
+    _stop(pids, "master")
+    _save_pids(pids)
+    print("local master down")
+
+
+def agent_up(a):
+    pids = _pids()
+    name = a.agent_name or f"{len([k for k in pids if k.startswith('agent-')])}"
+    _start_agent(name, a.master_url or a.master, a, pids)
+    _save_pids(pids)
+    print(f"local agent {name} up (master {a.master_url or a.master})")
+
+
+def agent_down(a):
+    pids = _pids()
+    names = [k for k in pids if k.startswith("agent-")] if a.all else \
+        [a.agent_name if a.agent_name.startswith("agent-") else f"agent-{a.agent_name}"]
+    for n in names:
+        _stop(pids, n)
+    _save_pids(pids)
+    print(f"stopped {', '.join(names) or 'no agents'}")
+
+
+def local_logs(a):
+    """``det deploy local logs``: the local master's log (follows unless --no-follow)."""
+    f = _local_dir() / (f"agent-{a.agent_name}.log" if a.agent_name else "master.log")
+    if not f.exists():
+        raise SystemExit(f"no log at {f}")
+    with open(f) as fh:
+        sys.stdout.write(fh.read())
+        sys.stdout.flush()
+        while not a.no_follow:
+            line = fh.readline()
+            if line:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                time.sleep(0.5)
 
 
 # ------------------------------------------------------------------------------------ parser
@@ -571,12 +674,34 @@ def build_parser() -> argparse.ArgumentParser:
     loc = dp.add_parser("local").add_subparsers(dest="verb", required=True)
     up = loc.add_parser("cluster-up")
     up.add_argument("--master-port", type=int, default=8080)
+    up.add_argument("--master-config-path", default=None, help="master configuration (YAML)")
     up.add_argument("--agents", type=int, default=1)
     up.add_argument("--no-gpu", action="store_true")
     up.add_argument("--cpu-slots", type=int, default=8)
     up.add_argument("--scheduler", default="priority", choices=["priority", "fair_share", "round_robin"])
     up.set_defaults(fn=cluster_up)
     loc.add_parser("cluster-down").set_defaults(fn=cluster_down)
+    mu = loc.add_parser("master-up")
+    mu.add_argument("--master-port", type=int, default=8080)
+    mu.add_argument("--master-config-path", default=None)
+    mu.add_argument("--scheduler", default="priority", choices=["priority", "fair_share", "round_robin"])
+    mu.set_defaults(fn=master_up)
+    loc.add_parser("master-down").set_defaults(fn=master_down)
+    au = loc.add_parser("agent-up")
+    au.add_argument("master_url", nargs="?", default=None)
+    au.add_argument("--agent-name", default=None)
+    au.add_argument("--no-gpu", action="store_true")
+    au.add_argument("--cpu-slots", type=int, default=8)
+    au.add_argument("--resource-pool", default=None)
+    au.set_defaults(fn=agent_up)
+    ad = loc.add_parser("agent-down")
+    ad.add_argument("--agent-name", default="0")
+    ad.add_argument("--all", action="store_true")
+    ad.set_defaults(fn=agent_down)
+    lg = loc.add_parser("logs")
+    lg.add_argument("--no-follow", action="store_true")
+    lg.add_argument("--agent-name", default=None)
+    lg.set_defaults(fn=local_logs)
     return p
 
 
