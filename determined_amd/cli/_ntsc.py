@@ -88,9 +88,9 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
         t = _wait_proxy(s, r["task_id"])
         print(f"Launched tensorboard {r['task_id']}: http://{t['proxy']['host']}:{t['proxy']['port']}/")
 
-    def tb_open(a):
+    def tb_open(a):  # through the master's task proxy, as the reference (master/internal/proxy)
         t = session(a).get(f"/api/v1/tasks/{a.task_id}")["task"]
-        print(f"http://{t['proxy']['host']}:{t['proxy']['port']}/" if t.get("proxy") else "not ready")
+        print(f"{a.master.rstrip('/')}/proxy/{a.task_id}/" if t.get("proxy") else "not ready")
 
     g = common(sub.add_parser("tensorboard"), "tensorboards", tb_start,
                [(("experiment_ids",), {"type": int, "nargs": "*"}),
@@ -108,7 +108,7 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
 
     def nb_open(a):
         t = session(a).get(f"/api/v1/tasks/{a.task_id}")["task"]
-        print(f"http://{t['proxy']['host']}:{t['proxy']['port']}/lab" if t.get("proxy") else "not ready")
+        print(f"{a.master.rstrip('/')}/proxy/{a.task_id}/lab" if t.get("proxy") else "not ready")
 
     nb = common(sub.add_parser("notebook"), "notebooks", nb_start, [(("--slots",), {"type": int, "default": 1})])
     o = nb.add_parser("open")

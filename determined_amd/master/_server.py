@@ -795,11 +795,66 @@ class _Handler(BaseHTTPRequestHandler):
     def log_message(self, fmt: str, *args: Any) -> None:
         logger.debug("%s - " + fmt, self.address_string(), *args)
 
+    def _proxy(self, method: str, parsed: Any, raw: bytes) -> None:
+        """``/proxy/<task_id>/<path>``: forward the request to the task's registered service
+        (notebook / TensorBoard / any NTSC that posted ``/api/v1/tasks/<id>/proxy``), as the
+        reference master's task proxy (``master/internal/proxy``) -- plain HTTP, no websockets."""
+        import http.client
+
+        parts = parsed.path.split("/", 3)  # ['', 'proxy', task_id, rest]
+        task_id = parts[2] if len(parts) > 2 else ""
+        rest = "/" + (parts[3] if len(parts) > 3 else "")
+        iam = self.master.iam if self.master else None
+        try:
+            if iam is not None:
+                auth = self.headers.get("Authorization")
+                if auth is None:  # browsers: the session token as a cookie
+                    for c in (self.headers.get("Cookie") or "").split(";"):
+                        k, _, v = c.strip().partition("=")
+                        if k == "auth":
+                            auth = f"Bearer {v}"
+                iam.set_current(iam.authenticate(auth))
+            row = self.master.db.one("SELECT proxy FROM tasks WHERE id=?", [task_id]) if self.master else None
+            px = (row or {}).get("proxy")
+            if not px or not px.get("port"):
+                raise HTTPError(404, f"task {task_id} has no proxied service (yet)")
+            conn = http.client.HTTPConnection(px.get("host") or "127.0.0.1", int(px["port"]), timeout=60)
+            hdrs = {k: v for k, v in self.headers.items() if k.lower() not in ("host", "authorization", "content-length",
+                                                                             "connection")}
+            conn.request(method, rest + (f"?{parsed.query}" if parsed.query else ""), body=raw or None, headers=hdrs)
+            resp = conn.getresponse()
+            data = resp.read()
+            self.send_response(resp.status)
+            for k, v in resp.getheaders():
+                if k.lower() not in ("transfer-encoding", "connection", "content-length"):
+                    self.send_header(k, v)
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+            conn.close()
+        except (HTTPError, AuthError) as e:
+            data = json.dumps({"error": e.message}).encode()
+            self.send_response(e.status)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        except OSError as e:
+            data = json.dumps({"error": f"proxied service unreachable: {e}"}).encode()
+            self.send_response(502)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
     def _dispatch(self, method: str) -> None:
         parsed = urllib.parse.urlparse(self.path)
         q = {k: v[-1] for k, v in urllib.parse.parse_qs(parsed.query).items()}
         n = int(self.headers.get("Content-Length") or 0)
         raw = self.rfile.read(n) if n else b""
+        if parsed.path.startswith("/proxy/"):
+            self._proxy(method, parsed, raw)
+            return
         status, ctype = 200, "application/json"
         try:
             iam = self.master.iam if self.master else None
