@@ -76,10 +76,13 @@ class Agent:
         self._stop = threading.Event()
 
     def register(self) -> None:
+        # `running`: the allocations this agent process still runs -- after an agent restart the
+        # master fails the ones it lost (their trials restart under max_restarts)
         self.session.post("/api/v1/agents/register", {"agent_id": self.agent_id, "slots": len(self.devices),
                                                       "host": self.host, "devices": self.devices,
                                                       "gpu": self.use_gpu, "label": self.label,
-                                                      "resource_pool": self.resource_pool})
+                                                      "resource_pool": self.resource_pool,
+                                                      "running": sorted(self.tasks)})
         logger.info(f"agent {self.agent_id} registered {len(self.devices)} {'GPU' if self.use_gpu else 'CPU'} slots")
 
     def run(self) -> None:

@@ -832,9 +832,22 @@ class Master:
 
     # ================================================================ agents
     def register_agent(self, agent_id: str, slots: int, host: str = "127.0.0.1", devices: Optional[List[Any]] = None,
-                       gpu: bool = False, label: str = "", resource_pool: Optional[str] = None) -> Dict[str, Any]:
+                       gpu: bool = False, label: str = "", resource_pool: Optional[str] = None,
+                       running: Optional[List[str]] = None) -> Dict[str, Any]:
         with self.lock:
             existing = self.agents.get(agent_id)
+            if existing is not None and running is not None:
+                # a re-registering agent lists what it still runs: allocations it was given and no
+                # longer knows (its process restarted) are lost, like a lost agent's (reference
+                # test_agent_restart: without container reattach the trial restarts)
+                alive = set(running)
+                queued = {c.get("allocation_id") for c in existing.get("queue", []) if c.get("type") == "start"}
+                for a in list(self.allocations.values()):
+                    if a.state == "RUNNING" and a.id not in alive and a.id not in queued and \
+                            any(x[0] == agent_id for x in a.assignment):
+                        logger.warning(f"agent {agent_id} restarted without allocation {a.id}: marking it lost")
+                        a.exit_codes[agent_id] = -1
+                        self._finish_allocation(a)
             pool = resource_pool or (existing or {}).get("resource_pool") or self.sched.default_compute
             if pool not in self.sched.pools:
                 raise ValueError(f"resource pool {pool!r} does not exist (pools: {sorted(self.sched.pools)})")

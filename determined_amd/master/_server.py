@@ -515,7 +515,7 @@ def build_routes(m: Master) -> List[Route]:
     @route("POST", "/api/v1/agents/register")
     def reg_agent(q, b):
         return m.register_agent(b["agent_id"], int(b["slots"]), b.get("host", "127.0.0.1"), b.get("devices"),
-                                bool(b.get("gpu")), b.get("label", ""), b.get("resource_pool"))
+                                bool(b.get("gpu")), b.get("label", ""), b.get("resource_pool"), b.get("running"))
 
     @route("GET", r"/api/v1/agents/([^/]+)/work")
     def agent_work(q, b, agent_id):

@@ -138,3 +138,25 @@ def test_test_one_batch_runs_a_trial_locally(tmp_path, monkeypatch):
         assert len(calls) == 1
     finally:
         sys.path.pop(0)
+
+
+def test_agent_restart_marks_lost_allocations(pooled):
+    """An agent that re-registers without an allocation it was running (its process restarted:
+    reference e2e test_agent_restart without reattach) gets that allocation failed, so trials
+    restart under max_restarts instead of hanging; a plain reconnect listing it changes nothing."""
+    srv, s = pooled
+    m = srv.master
+    s.post("/api/v1/agents/register", {"agent_id": "n", "slots": 8, "resource_pool": "train"})
+    t1 = s.post("/api/v1/commands", {"command": ["sleep", "60"], "slots": 1})["task_id"]
+    t2 = s.post("/api/v1/commands", {"command": ["sleep", "60"], "slots": 1})["task_id"]
+    with m.lock:
+        m._schedule()
+    a1, a2 = (next(a for a in m.allocations.values() if a.task_id == t) for t in (t1, t2))
+    assert len(s.get("/api/v1/agents/n/work", params={"timeout_seconds": 0})["commands"]) == 2
+    for a in (a1, a2):
+        s.post("/api/v1/agents/n/events", {"type": "started", "allocation_id": a.id})
+    s.post("/api/v1/agents/register", {"agent_id": "n", "slots": 8, "resource_pool": "train", "running": [a1.id, a2.id]})
+    assert a1.state == "RUNNING" and a2.state == "RUNNING"
+    s.post("/api/v1/agents/register", {"agent_id": "n", "slots": 8, "resource_pool": "train", "running": [a2.id]})
+    assert a1.state == "TERMINATED" and a2.state == "RUNNING"
+    assert s.get(f"/api/v1/tasks/{t1}")["task"]["exit_code"] == -1
