@@ -46,10 +46,11 @@ def parse() -> argparse.Namespace:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
-    # 1024 images per GPU (~120 GB of the 288 GB HBM3E): same box, current kernels, 20 steps:
-    # 256 -> 12,526, 512 -> 14,050, 1024 -> 15,180 samples/s (profiles/resnet50_batch_sweep_1gpu.jsonl);
-    # the larger pixel count fills the 14x14 / 7x7 layers' tiles across the 256 CUs
-    p.add_argument("--batch", type=int, default=1024, help="per-GPU batch size")
+    # 2048 images per GPU (78.5 GiB peak of the 288 GB HBM3E): one box, MIOpen immediate mode,
+    # 1024 -> 14,945, 1536 -> 15,532, 2048 -> 15,679 samples/s (profiles/resnet50_batch_sweep_immediate_1gpu.txt;
+    # earlier: 256 -> 12,526, 512 -> 14,050); the larger pixel count fills the 14x14 / 7x7 layers'
+    # tiles across the 256 CUs
+    p.add_argument("--batch", type=int, default=2048, help="per-GPU batch size")
     p.add_argument("--variant", default="bf16_master", choices=["bf16_master", "amp", "bf16_fp32bn"])
     p.add_argument("--no-harness", action="store_true", help="bypass the PyTorchTrial controller")
     p.add_argument("--bucket-mb", type=float, default=16.0)
@@ -57,7 +58,11 @@ def parse() -> argparse.Namespace:
     p.add_argument("--save-tune-db", default="", help="write the per-layer conv kernel choices after warm-up")
     p.add_argument("--no-pretune", action="store_true",
                    help="pick conv kernels inside the first warm-up step instead of a separate no-sync pass")
-    p.add_argument("--conv-benchmark", type=int, default=1,
+    # MIOpen immediate mode takes the solvers recorded in the in-tree find-db (searched once on an
+    # MI355X, scripts/gpu_finddb.sh) without re-running the search on every fresh box: batch 2048
+    # starts in ~11 s instead of ~300 s at the same throughput (15,957 / 15,980 vs 15,910 / 15,957
+    # samples/s, profiles/resnet50_b2048_finddb_vs_immediate_1gpu.txt)
+    p.add_argument("--conv-benchmark", type=int, default=0,
                    help="1: let MIOpen search for the fastest conv solvers (torch.backends.cudnn.benchmark)")
     return p.parse_args()
 

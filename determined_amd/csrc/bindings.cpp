@@ -937,6 +937,7 @@ int64_t conv_sk_timeouts(const at::Tensor& like, bool reset) {
 bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg, int64_t stride, int64_t pad) {
   if (cfg < 0) cfg = damd_conv_default_cfg(static_cast<int>(w.size(0)), 0);
   return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+         x.numel() * 2 < 0xF0000000LL &&  // 32-bit buffer offsets in the kernels (conv_igemm.hip)
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
          w.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.size(1) == x.size(1) &&
          damd_conv_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(w.size(2)),

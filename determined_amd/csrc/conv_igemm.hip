@@ -59,6 +59,7 @@ struct Geo {
   // [N][OHf][OWf] grid and output pixel m = (n, i, j) of the OH x OW grid goes to (n, 2i + oa, 2j + ob)
   // (one phase of a stride-2 input gradient, conv_phase_launch)
   int ost, oa, ob, OHf, OWf;
+  uint32_t xbytes;   // input tensor bytes (< 0xF0000000: 32-bit buffer offsets, damd_conv_fwd_launch)
 };
 
 __device__ __forceinline__ int64_t out_row(const Geo& g, int64_t m) {
@@ -75,8 +76,19 @@ __device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
 
 __device__ __forceinline__ int swz(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
 
+// compile-time integer tag (ring slots of the unrolled main loops)
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
 __device__ __forceinline__ void dma16(const void* src, bf16_t* lds_base) {
   __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+// the buffer form: 16 bytes from rsrc + voff (per lane) + soff (wave-uniform) to LDS
+__device__ __forceinline__ void dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff, bf16_t* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_base, 16, voff, soff, 0, 0);
 }
 
 // A-operand row (output channel within the wave's co range) of fragment i for fragment row rho:
@@ -476,7 +488,9 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STAGE + PARAMS];
   float* prm = reinterpret_cast<float*>(lds + NST * STAGE);
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index as a provably uniform (SGPR) value: the LDS-DMA destinations derived from it go
+  // to M0 without a v_readfirstlane per DMA
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int rho = lane & 15, lg = lane >> 4;
   const int wco0 = (wave % WCO) * TCO, wp0 = (wave / WCO) * TP;
 
@@ -488,6 +502,14 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   const Plan plan = make_plan(grp, g.groups, g.ptiles, g.ksteps, SK);
   const int items = plan_units(plan, g.ksteps);
   const int64_t Ktot = static_cast<int64_t>(g.ksteps) * kBK;
+  // LDS-DMA through buffer resources (buffer_load_dwordx4 ... lds): a lane's source is a 32-bit
+  // byte offset (VGPR) plus a wave-uniform k-step offset (SGPR), so a DMA costs no 64-bit VALU
+  // address arithmetic; an out-of-range offset (a tap outside the image) reads zeros.  The host
+  // keeps both tensors below 0xF0000000 bytes (damd_conv_fwd_launch).
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(w), 0, static_cast<int>(g.K * Ktot * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(x), 0, static_cast<int>(g.xbytes), 0x00020000);
   if (EPI >= kEpiBnbM) {  // visible to every wave after the main loop's first barrier
     for (int t = threadIdx.x; t < BCO; t += NT) {
       const int co = ct * BCO + t;
@@ -499,21 +521,21 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
 
   // ---- DMA lane roles: lane -> (row within its 8-row piece, 16-byte slot)
   const int prow = lane >> 3, slot = lane & 7;
-  const bf16_t* wsrc[NIW];
+  uint32_t wvoff[NIW];  // byte offset of the lane's weight chunk at k-step 0
 #pragma unroll
   for (int i = 0; i < NIW; ++i) {
     const int co = 8 * (wave + NW * i) + prow;
-    wsrc[i] = w + (static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3);
+    wvoff[i] = static_cast<uint32_t>(((static_cast<int64_t>(ct) * BCO + co) * Ktot + ((slot ^ swz(co)) << 3)) * 2);
   }
   // pixel rows, per tile: element offset of the row's tap-(0,0) input pixel (+ its DMA chunk;
   // may lie outside the image -- only dereferenced for valid taps) and a bit mask of the taps
   // r*S + s that fall inside the image.  Per k-step the source is then one 64-bit add of a
   // wave-uniform tap/channel offset and a bit test (the per-k-step im2col arithmetic was ~4
   // VALU instructions per MFMA in the PMC counters).
-  int64_t xbase[NIX];
+  int32_t xbase[NIX];  // bytes (may be negative: only used for taps inside the image)
   uint32_t vmask[NIX];
   const int OHW = g.OH * g.OW;
-  auto tile_rows = [&](int pt) {
+  auto tile_rows = [&](int pt) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
       const int p = 8 * (wave + NW * i) + prow;
@@ -522,7 +544,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       const int rem = m - n * OHW;
       const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
       const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
-      xbase[i] = ((static_cast<int64_t>(n) * g.H + ih0) * g.W + iw0) * g.C + ((slot ^ swz(p)) << 3);
+      xbase[i] = static_cast<int32_t>((((static_cast<int64_t>(n) * g.H + ih0) * g.W + iw0) * g.C + ((slot ^ swz(p)) << 3)) * 2);
       uint32_t bits = 0;
       if (m < g.M) {
         for (int r = 0; r < g.R; ++r) {
@@ -540,7 +562,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   bf16x8 py[PRO ? NIX : 1], pr[PRO ? NIX : 1];
   float4 psc[2], psh[2], prs[2];
   int p_pt = 0, p_cb = 0;
-  auto load_px = [&](int pt, int cb) {
+  auto load_px = [&](int pt, int cb) __attribute__((always_inline)) {
     p_pt = pt;
     p_cb = cb;
     const int cofs = cb * kBK + (slot << 3);
@@ -561,7 +583,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
   };
   // transform the staged rows into LDS slot `stage` (+ a / mask stores by co tile 0)
-  auto store_px = [&](int stage) {
+  auto store_px = [&](int stage) __attribute__((always_inline)) {
     bf16_t* sx = lds + stage * STAGE + BCO * kBK;
     const float sc[8] = {psc[0].x, psc[0].y, psc[0].z, psc[0].w, psc[1].x, psc[1].y, psc[1].z, psc[1].w};
     const float sh[8] = {psh[0].x, psh[0].y, psh[0].z, psh[0].w, psh[1].x, psh[1].y, psh[1].z, psh[1].w};
@@ -607,7 +629,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   seg_enter(lc, plan, g.ksteps);
   int l_cb = 0, l_r = 0, l_s = 0;
   bool l_new = true;
-  auto seed = [&]() {  // k-step lc.k = (r * S + s) * cblk + cb
+  auto seed = [&]() __attribute__((always_inline)) {  // k-step lc.k = (r * S + s) * cblk + cb
     l_cb = lc.k % g.cblk;
     const int rs = lc.k / g.cblk;
     l_s = rs % g.S;
@@ -615,21 +637,21 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     l_new = true;
   };
   seed();
-  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_rows) + (slot << 3);
-  auto issue = [&](int stage) {
+  auto issue = [&](int stage) __attribute__((always_inline)) {
     bf16_t* sw = lds + stage * STAGE;
     const int pt = lc.pt;
     if (!PRO && l_new) tile_rows(pt);
     l_new = false;
+    const int wk = lc.k * kBK * 2;  // wave-uniform byte offset of this k-step in a weight row
 #pragma unroll
-    for (int i = 0; i < NIW; ++i) dma16(wsrc[i] + lc.k * kBK, sw + 8 * (wave + NW * i) * kBK);
+    for (int i = 0; i < NIW; ++i) dma16b(rs_w, wvoff[i], wk, sw + 8 * (wave + NW * i) * kBK);
     if (!PRO) {
       const int tap = l_r * g.S + l_s;
-      const int64_t soff = static_cast<int64_t>(l_r * g.W + l_s) * g.C + l_cb * kBK;  // wave-uniform
+      const int soff = ((l_r * g.W + l_s) * g.C + l_cb * kBK) * 2;  // wave-uniform, bytes
 #pragma unroll
       for (int i = 0; i < NIX; ++i) {
-        const bf16_t* src = (vmask[i] >> tap) & 1u ? x + (xbase[i] + soff) : zero;
-        dma16(src, sw + (BCO + 8 * (wave + NW * i)) * kBK);
+        const uint32_t off = (vmask[i] >> tap) & 1u ? static_cast<uint32_t>(xbase[i] + soff) : 0xFFFFFFF0u;
+        dma16b(rs_x, off, 0, sw + (BCO + 8 * (wave + NW * i)) * kBK);
       }
     } else {
       load_px(pt, l_cb);
@@ -678,6 +700,26 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
   }
 
+  // The main loops run NST items per trip with the ring slot of each a compile-time constant
+  // (step(IC<S>)): every fragment read is then `ds_read_b128 off[lane] offset:S*STAGE` with no VALU
+  // address arithmetic (a runtime slot cost two VALU instructions per read -- the kernels are
+  // VALU-issue-bound, profiles/conv3x3_pmc_valu_bound_b1024_1gpu.txt).
+  auto tile_done = [&](Cursor& cc) __attribute__((always_inline)) {
+    if (++cc.k == cc.kend) {
+      const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
+      if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
+        sk_publish<FI, FJ, NT>(acc, sk, rid);
+      } else {
+        if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.ksteps, g.ctiles, ct);
+        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, cc.pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      seg_next(cc, plan, g.ksteps);
+    }
+  };
   if constexpr (SCH == 3) {
     // Software-pipelined k-steps: the fragments of each k-half are read from LDS while the other
     // half's MFMAs run -- the item's second half during its first half's MFMAs, the NEXT item's
@@ -687,14 +729,15 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     // (lgkmcnt) and on the DMA / operand registers of item it+1 (vmcnt), so item it+2 may then be
     // issued into slot (it+2) % NST and item it+1's operand stored (PRO) into slot (it+1) % NST.
     s8 fa[2][FI], fb[2][FJ];
-    auto read_half = [&](int slot, int kk) {
-      const bf16_t* sw = lds + slot * STAGE;
+    auto read_half = [&](auto SI, int kk) __attribute__((always_inline)) {
+      constexpr int S = decltype(SI)::value;
+      const bf16_t* sw = lds + S * STAGE;
 #pragma unroll
       for (int i = 0; i < FI; ++i) fa[kk][i] = *reinterpret_cast<const s8*>(sw + aoff[kk][i]);
 #pragma unroll
       for (int j = 0; j < FJ; ++j) fb[kk][j] = *reinterpret_cast<const s8*>(sw + boff[kk][j]);
     };
-    auto mfma_half = [&](int kk) {
+    auto mfma_half = [&](int kk) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -717,37 +760,31 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      read_half(0, 0);
+      read_half(IC<0>{}, 0);
     }
     Cursor cc{0, 0, 0, 0, 0};
     seg_enter(cc, plan, g.ksteps);
-    for (int it = 0; it < items; ++it) {
-      read_half(it % NST, 1);
+    auto step = [&](auto SI, int it) __attribute__((always_inline)) {
+      constexpr int S = decltype(SI)::value;
+      read_half(SI, 1);
       mfma_half(0);
       if (it + 1 < items) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // item it+1: DMA (+ operand registers, PRO)
-        if (PRO) store_px((it + 1) % NST);
+        if (PRO) store_px((S + 1) % NST);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot it (+ its stores)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (it + 2 < items) issue((it + 2) % NST);
-        read_half((it + 1) % NST, 0);
+        if (it + 2 < items) issue((S + 2) % NST);
+        read_half(IC<(S + 1) % NST>{}, 0);
       }
       mfma_half(1);
-    if (++cc.k == cc.kend) {
-      const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
-      if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
-        sk_publish<FI, FJ, NT>(acc, sk, rid);
-      } else {
-        if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.ksteps, g.ctiles, ct);
-        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, cc.pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
-      }
-#pragma unroll
-      for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-      seg_next(cc, plan, g.ksteps);
-    }
+      tile_done(cc);
+    };
+    for (int it0 = 0; it0 < items; it0 += NST) {
+      step(IC<0>{}, it0);
+      if (it0 + 1 < items) step(IC<1>{}, it0 + 1);
+      if constexpr (NST > 2) if (it0 + 2 < items) step(IC<2 % NST>{}, it0 + 2);
+      if constexpr (NST > 3) if (it0 + 3 < items) step(IC<3 % NST>{}, it0 + 3);
     }
   } else {
     if (PRO) {
@@ -766,13 +803,14 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
     }
     Cursor cc{0, 0, 0, 0, 0};
     seg_enter(cc, plan, g.ksteps);
-    for (int it = 0; it < items; ++it) {
+    auto step = [&](auto SI, int it) __attribute__((always_inline)) {
+      constexpr int S = decltype(SI)::value;
       if (PRO) {
         // weights of item it, input registers of item it+1 and this wave's LDS writes of item it
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (it + 1 < items) store_px((it + 1) % NST);
-        if (it + 2 < items) issue((it + 2) % NST);
+        if (it + 1 < items) store_px((S + 1) % NST);
+        if (it + 2 < items) issue((S + 2) % NST);
       } else {
         // retire slot it: the DMAs of the (at most NST - 2) later slots already issued may stay in flight
         const int ahead = items - 1 - it;
@@ -780,9 +818,9 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
         else if (NST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // slot it landed for every wave; slot it-1 is no longer read
-        if (it + NST - 1 < items) issue((it + NST - 1) % NST);
+        if (it + NST - 1 < items) issue((S + NST - 1) % NST);
       }
-      const bf16_t* sw = lds + (it % NST) * STAGE;
+      const bf16_t* sw = lds + S * STAGE;
       if (SCH == 0) {
   #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -814,20 +852,13 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
             for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
         if (SCH == 2) __builtin_amdgcn_s_setprio(0);
       }
-      if (++cc.k == cc.kend) {
-        const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.ksteps);
-        if (!whole) {  // HEAD / middle segment: hand the partial tile to the block that finishes it
-          sk_publish<FI, FJ, NT>(acc, sk, rid);
-        } else {
-          if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.ksteps, g.ctiles, ct);
-          epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, cc.pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
-        }
-  #pragma unroll
-        for (int i = 0; i < FI; ++i)
-  #pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        seg_next(cc, plan, g.ksteps);
-      }
+      tile_done(cc);
+    };
+    for (int it0 = 0; it0 < items; it0 += NST) {
+      step(IC<0>{}, it0);
+      if (it0 + 1 < items) step(IC<1>{}, it0 + 1);
+      if constexpr (NST > 2) if (it0 + 2 < items) step(IC<2 % NST>{}, it0 + 2);
+      if constexpr (NST > 3) if (it0 + 3 < items) step(IC<3 % NST>{}, it0 + 3);
     }
   }
 
@@ -1847,6 +1878,9 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
     g.OW = W;
   }
   g.M = static_cast<int64_t>(N) * g.OH * g.OW;
+  const int64_t xbytes = static_cast<int64_t>(N) * H * W * C * 2;
+  if (xbytes >= 0xF0000000LL || static_cast<int64_t>(K) * R * S * C * 2 >= 0xF0000000LL) return -7;
+  g.xbytes = static_cast<uint32_t>(xbytes);
   g.cblk = C / kBK;
   g.ksteps = R * S * g.cblk;
   g.ptiles = static_cast<int>((g.M + c.bp - 1) / c.bp);

@@ -9,6 +9,7 @@ math (that is what the CPU test-suite exercises).
 """
 
 import importlib
+import importlib.util
 import os
 from typing import Any, Optional
 
@@ -23,7 +24,14 @@ def _load() -> Optional[Any]:
     try:
         import torch  # noqa: F401  (loads libtorch/libamdhip64 before the extension)
 
-        _ext = importlib.import_module("determined_amd.ops._hip_ops")
+        alt = os.environ.get("DAMD_HIP_OPS_PATH")  # A/B runs: another build of the same extension
+        if alt:
+            spec = importlib.util.spec_from_file_location("determined_amd.ops._hip_ops", alt)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)  # type: ignore[union-attr]
+            _ext = mod
+        else:
+            _ext = importlib.import_module("determined_amd.ops._hip_ops")
     except BaseException as e:  # ImportError, OSError from a bad .so, ...
         _err = e
         if os.environ.get("DAMD_AUTOBUILD", "0") == "1":
