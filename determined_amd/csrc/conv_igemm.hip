@@ -890,7 +890,7 @@ constexpr int kHaloProRows = 6;  // register-staged halo rows per lane: HR <= 6 
 template <int BCO, int BP, int WCO, int NW, int EPI, int SK = 0, int PRO = 0>
 __global__ void __launch_bounds__(64 * NW, 2)
 conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk, ProArgs pa, int sch) {
+               float* __restrict__ part, Geo g, EpiArgs ea, int HR, SkArgs sk, ProArgs pa) {
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int NT = 64 * NW;
   constexpr int WP = NW / WCO;
@@ -905,6 +905,11 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   bf16_t* wts = lds + 2 * HSLOT;    // [3][BCO][64]
   float* prm = reinterpret_cast<float*>(wts + 3 * WSLOT);
   float* pprm = prm + 3 * BCO;      // PRO: [3][C] per input channel scale / shift / rscale
+  // one 128-byte zero row after the parameters (host: halo_lds_bytes): the fragment source of taps
+  // that fall outside the image
+  bf16_t* zrow = reinterpret_cast<bf16_t*>(pprm + (PRO ? 3 * g.C : 0));
+  static_assert(sizeof(bf16x8) == 16, "zero row store");
+  if (threadIdx.x < 8) *reinterpret_cast<bf16x8*>(zrow + 8 * threadIdx.x) = bf16x8{};
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rho = lane & 15, lg = lane >> 4;
@@ -933,8 +938,8 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     }
     // the first flush() (item 0's halo, before the main loop's first barrier) reads channels
     // staged by other waves (threads t < C: with C = 64 wave 0 alone writes every parameter)
-    __syncthreads();
   }
+  __syncthreads();  // prologue parameters and the zero row
   const int prow = lane >> 3, slot = lane & 7;
   const bf16_t* wsrc[NIW];
 #pragma unroll
@@ -951,7 +956,7 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   int64_t p_f0 = 0;
   int p_cb = 0;
   bool p_pending = false;
-  auto flush = [&]() {
+  auto flush = [&]() __attribute__((always_inline)) {
     if (!PRO || !p_pending) return;
     p_pending = false;
     const float* sc = pprm + p_cb * kBK + (slot << 3);
@@ -991,7 +996,7 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   Cursor lc{0, 0, 0, 0, 0};
   seg_enter(lc, plan, g.cblk);
   int l_tap = 0, l_halo = 0;
-  auto issue = [&](int wslot) {
+  auto issue = [&](int wslot) __attribute__((always_inline)) {
     const int l_cb = lc.k;
     if (l_tap == 0) {  // stage this tile's halo for channel block l_cb
       const int64_t f0 = static_cast<int64_t>(lc.pt) * BP - g.W - 1;
@@ -1052,9 +1057,38 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
   if (items > 1) issue(1);
   Cursor cc{0, 0, 0, 0, 0};
   seg_enter(cc, plan, g.cblk);
-  int c_tap = 0, c_halo = 0;
-  bool c_first = true;  // first item of a segment: per-pixel tap masks of its tile
-  for (int it = 0; it < items; ++it) {
+  int c_halo = 0;
+  bool c_first = true;  // first unit of a segment: per-pixel tap masks of its tile
+
+  // Lane-constant LDS byte addresses, computed once: the weight fragments of ring slot 0 (the slot
+  // of a tap is compile-time below, so it lands in the ds_read offset field), the halo fragment rows
+  // (the halo slot and the tap's row shift are wave-uniform per tap: one v_add per fragment), and the
+  // zero row an out-of-image tap reads instead of selecting zeros into the fragment dwords.
+  const char* lds_c = reinterpret_cast<const char*>(lds);
+  const uint32_t wts_b = static_cast<uint32_t>(reinterpret_cast<const char*>(wts) - lds_c);
+  const uint32_t zrow_b = static_cast<uint32_t>(reinterpret_cast<const char*>(zrow) - lds_c);
+  uint32_t aoff[2][FI], zoff[2];
+  int brow[FJ];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wco0 + a_row(i, rho);
+      aoff[kk][i] = wts_b + 2u * static_cast<uint32_t>(row * kBK + (((kk * 4 + lg) ^ swz(row)) << 3));
+    }
+    zoff[kk] = zrow_b + (static_cast<uint32_t>(kk * 4 + lg) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) brow[j] = wp0 + 16 * j + rho;
+  // LDS byte offsets from the dynamic LDS base (the halo ring starts there)
+  auto ld_s8 = [&](uint32_t off) __attribute__((always_inline)) {
+    return *reinterpret_cast<const s8*>(lds_c + off);
+  };
+
+  // One item = one tap of one 64-channel unit; items come in units of 9 taps, so the weight ring
+  // slot (item % 3) and the tap's (r, s) are compile-time in the 9-way unrolled unit body.
+  auto tap = [&](auto TT, int it, int hrow0) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value;
     // the next item's DMAs may stay in flight (a halo issued with it is over-waited: correct;
     // a register-staged halo (PRO) is waited for here and written to LDS by flush() below)
     if (PRO) {
@@ -1066,7 +1100,27 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
     }
     __builtin_amdgcn_s_barrier();
     flush();  // the halo of item it+1 (slot free: last read two units ago)
-    if (it + 2 < items) issue((it + 2) % 3);
+    if (it + 2 < items) issue((T + 2) % 3);
+    const int rb = hrow0 + (T / 3) * g.W + (T % 3);  // wave-uniform row shift of this tap
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s8 a[FI], b[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) a[i] = ld_s8(aoff[kk][i] + 2u * (T % 3) * WSLOT);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int row = brow[j] + rb;
+        const uint32_t hb = 2u * static_cast<uint32_t>(row * kBK + (((kk * 4 + lg) ^ (row & 7)) << 3));
+        b[j] = ld_s8(((vm[j] >> T) & 1u) ? hb : zoff[kk]);
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+  };
+
+  for (int it0 = 0; it0 < items; it0 += 9) {
     const int64_t pt = cc.pt;
     if (c_first) {
       c_first = false;
@@ -1089,74 +1143,31 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_
         vm[j] = bits;
       }
     }
-    const bf16_t* sw = wts + (it % 3) * WSLOT;
-    const bf16_t* sh = halo + (c_halo & 1) * HSLOT;
-    const int rowoff = (c_tap / 3) * g.W + (c_tap % 3);
-    auto read_a = [&](int kk, int i) {
-      const int row = wco0 + a_row(i, rho);
-      return *reinterpret_cast<const s8*>(sw + row * kBK + (((kk * 4 + lg) ^ swz(row)) << 3));
-    };
-    auto read_b = [&](int kk, int j) {
-      const int row = wp0 + 16 * j + rho + rowoff;
-      return *reinterpret_cast<const s8*>(sh + row * kBK + (((kk * 4 + lg) ^ (row & 7)) << 3));
-    };
-    if (sch == 1) {  // both k-halves' fragment reads first: the second half's reads overlap the first's MFMAs
-      s8 a[2][FI], b[2][FJ];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int i = 0; i < FI; ++i) a[kk][i] = read_a(kk, i);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) b[kk][j] = read_b(kk, j);
+    const int hrow0 = (c_halo & 1) * HR;  // halo slot as a row offset (HR % 8 == 0: same swizzle)
+    tap(IC<0>{}, it0, hrow0);
+    tap(IC<1>{}, it0 + 1, hrow0);
+    tap(IC<2>{}, it0 + 2, hrow0);
+    tap(IC<3>{}, it0 + 3, hrow0);
+    tap(IC<4>{}, it0 + 4, hrow0);
+    tap(IC<5>{}, it0 + 5, hrow0);
+    tap(IC<6>{}, it0 + 6, hrow0);
+    tap(IC<7>{}, it0 + 7, hrow0);
+    tap(IC<8>{}, it0 + 8, hrow0);
+    ++c_halo;
+    if (++cc.k == cc.kend) {
+      const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.cblk);
+      if (!whole) {
+        sk_publish<FI, FJ, NT>(acc, sk, rid);
+      } else {
+        if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.cblk, g.ctiles, ct);
+        epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
       }
-      if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half of each SIMD pair
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j)
-          if (!((vm[j] >> c_tap) & 1u)) b[kk][j] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[kk][i], b[kk][j], acc[i][j]);
-      }
-      if (wave >= NW / 2) __builtin_amdgcn_s_setprio(0);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        s8 a[FI], b[FJ];
-#pragma unroll
-        for (int i = 0; i < FI; ++i) a[i] = read_a(kk, i);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) {
-          const s8 v = read_b(kk, j);
-          const bool ok = (vm[j] >> c_tap) & 1u;
-          b[j] = ok ? v : s8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
-      }
-    }
-    if (++c_tap == 9) {
-      c_tap = 0;
-      ++c_halo;
-      if (++cc.k == cc.kend) {
-        const bool whole = !SK || cc.run == 0 || (cc.run == 2 && cc.kend == g.cblk);
-        if (!whole) {
-          sk_publish<FI, FJ, NT>(acc, sk, rid);
-        } else {
-          if (SK && cc.run == 2) sk_gather<FI, FJ, NT>(acc, sk, plan, cc.pt, g.cblk, g.ctiles, ct);
-          epi_store_tile<BCO, BP, FI, FJ, EPI>(acc, pt, ct, wco0, wp0, lg, rho, g, ea, prm, y, st_s, st_q);
-        }
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        seg_next(cc, plan, g.cblk);
-        c_first = true;
-      }
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      seg_next(cc, plan, g.cblk);
+      c_first = true;
     }
   }
   if (SUMS) epi_flush_sums<BCO, FI, WCO, NW>(st_s, st_q, lds, wave, lg, rho, wco0, grp, ct, g.K, part);
@@ -1746,7 +1757,7 @@ int halo_rows(int bp, int W) { return (bp + 2 * W + 2 + 7) / 8 * 8; }
 constexpr int kSkMaxBlocks = 4096;  // flag words the host keeps per device (damd_conv_sk_flag_words)
 
 int halo_lds_bytes(const Cfg& c, int W, int C = 0) {  // C > 0: + the prologue's per-channel parameters
-  return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4 + 3 * C * 4;
+  return (2 * halo_rows(c.bp, W) * kBK + 3 * c.bco * kBK) * 2 + 3 * c.bco * 4 + 3 * C * 4 + 128;  // + zero row
 }
 
 int blocks_per_cu(const Cfg& c, int W = 0) {
@@ -1794,15 +1805,6 @@ int damd_conv_supported(int C, int K, int R, int S, int stride, int pad, int W, 
   if (c.nst == 0)
     return R == 3 && S == 3 && stride == 1 && pad == 1 && W >= 1 && halo_lds_bytes(c, W) <= kHaloMaxLds;
   return 1;
-}
-
-// DAMD_HALO_SCH=1: the 3x3 halo kernel's all-reads-first k-step schedule (A/B switch)
-int halo_sch() {
-  static const int v = [] {
-    const char* e = getenv("DAMD_HALO_SCH");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 // DAMD_CONV_OVERSUB=k: k x the resident grid for the (non-stream-K) persistent configs, so blocks
@@ -1928,7 +1930,7 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   do {                                                                                                       \
     auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_, P_>;                                                  \
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa, halo_sch());  \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa);  \
   } while (0)
 #define H1(BCO, BP, WCO, NW, E, K_)                        \
   do {                                                     \
