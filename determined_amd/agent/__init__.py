@@ -73,6 +73,9 @@ class Agent:
         self.host = host or "127.0.0.1"
         self.label = label
         self.tasks: Dict[str, _Task] = {}
+        # allocations whose start command arrived but whose process is not up yet: listed as running
+        # from the moment the command is received, so a re-registration in between never loses them
+        self._starting: set = set()
         self._stop = threading.Event()
 
     def register(self) -> None:
@@ -82,7 +85,7 @@ class Agent:
                                                       "host": self.host, "devices": self.devices,
                                                       "gpu": self.use_gpu, "label": self.label,
                                                       "resource_pool": self.resource_pool,
-                                                      "running": sorted(self.tasks)})
+                                                      "running": sorted(set(self.tasks) | self._starting)})
         logger.info(f"agent {self.agent_id} registered {len(self.devices)} {'GPU' if self.use_gpu else 'CPU'} slots")
 
     def run(self) -> None:
@@ -101,6 +104,7 @@ class Agent:
                 continue
             for c in cmds:
                 if c["type"] == "start":
+                    self._starting.add(c["allocation_id"])
                     threading.Thread(target=self._run_task, args=(c,), daemon=True).start()
                 elif c["type"] == "kill":
                     self._kill(c["allocation_id"])
@@ -144,6 +148,7 @@ class Agent:
         aid = c["allocation_id"]
         t = _Task(c)
         self.tasks[aid] = t
+        self._starting.discard(aid)
         code = -1
         try:
             wd = self._prepare_workdir(c)

@@ -569,11 +569,11 @@ void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   a.H = H; a.T = T; a.scale_log2 = scale * kLog2e;
   dim3 grid((T + kFwdRows - 1) / kFwdRows, H, B);
   if (D == 64) {
-    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
+    if (causal) DAMD_LAUNCH((attn_fwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
+    else DAMD_LAUNCH((attn_fwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
   } else {
-    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
+    if (causal) DAMD_LAUNCH((attn_fwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
+    else DAMD_LAUNCH((attn_fwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
   }
   DAMD_CHECK_LAUNCH();
 }
@@ -590,10 +590,10 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
     const int64_t threads = rows * (D / 8);
     const int blocks = static_cast<int>((threads + 255) / 256);
     if (D == 64)
-      hipLaunchKernelGGL((attn_delta_kernel<64>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o), so,
+      DAMD_LAUNCH((attn_delta_kernel<64>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o), so,
                          static_cast<const bf16_t*>(dout), sdo, delta, H, T, rows);
     else
-      hipLaunchKernelGGL((attn_delta_kernel<128>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o),
+      DAMD_LAUNCH((attn_delta_kernel<128>), dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(o),
                          so, static_cast<const bf16_t*>(dout), sdo, delta, H, T, rows);
     DAMD_CHECK_LAUNCH();
   }
@@ -605,11 +605,11 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   a.H = H; a.T = T; a.scale = scale; a.scale_log2 = scale * kLog2e;
   dim3 grid((T + kBlk - 1) / kBlk, H, B);
   if (D == 64) {
-    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((attn_bwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
+    if (causal) DAMD_LAUNCH((attn_bwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
+    else DAMD_LAUNCH((attn_bwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
   } else {
-    if (causal) hipLaunchKernelGGL((attn_bwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
+    if (causal) DAMD_LAUNCH((attn_bwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
+    else DAMD_LAUNCH((attn_bwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
   }
   DAMD_CHECK_LAUNCH();
   DqArgs d;
@@ -619,11 +619,11 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   d.H = H; d.T = T; d.scale = scale; d.scale_log2 = scale * kLog2e;
   dim3 qgrid((T + kFwdRows - 1) / kFwdRows, H, B);
   if (D == 64) {
-    if (causal) hipLaunchKernelGGL((attn_dq_kernel<64, true>), qgrid, dim3(kThreads), 0, st, d);
-    else hipLaunchKernelGGL((attn_dq_kernel<64, false>), qgrid, dim3(kThreads), 0, st, d);
+    if (causal) DAMD_LAUNCH((attn_dq_kernel<64, true>), qgrid, dim3(kThreads), 0, st, d);
+    else DAMD_LAUNCH((attn_dq_kernel<64, false>), qgrid, dim3(kThreads), 0, st, d);
   } else {
-    if (causal) hipLaunchKernelGGL((attn_dq_kernel<128, true>), qgrid, dim3(kThreads), 0, st, d);
-    else hipLaunchKernelGGL((attn_dq_kernel<128, false>), qgrid, dim3(kThreads), 0, st, d);
+    if (causal) DAMD_LAUNCH((attn_dq_kernel<128, true>), qgrid, dim3(kThreads), 0, st, d);
+    else DAMD_LAUNCH((attn_dq_kernel<128, false>), qgrid, dim3(kThreads), 0, st, d);
   }
   DAMD_CHECK_LAUNCH();
 }

@@ -5,11 +5,13 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <vector>
 
 namespace damd {
+[[noreturn]] void launch_failed(hipError_t err, const char* func, const char* file, int line);  // common.h
 constexpr int kMaxGroups = 8;
 struct MTChunk {
   void* p;
@@ -142,6 +144,17 @@ extern "C" int damd_bias_grad_splits(int64_t, int);
 extern "C" void damd_bias_grad_launch(const void*, int64_t, int, int, float*, void*, int, hipStream_t);
 extern "C" void damd_gelu_fwd_launch(const void*, void*, int64_t, hipStream_t);
 extern "C" void damd_gelu_bwd_bias_launch(const void*, const void*, void*, int64_t, int, int, float*, hipStream_t);
+extern "C" void damd_debug_launch(float*, int, int, hipStream_t);
+
+// common.h: every DAMD_LAUNCH / DAMD_CHECK failure in the device TUs ends here and becomes a
+// c10::Error (Python RuntimeError) naming the launcher and source line.
+[[noreturn]] void damd::launch_failed(hipError_t err, const char* func, const char* file, int line) {
+  const char* base = std::strrchr(file, '/');
+  TORCH_CHECK(false, "determined_amd kernel launch failed in ", func, " (", base ? base + 1 : file, ":", line,
+              "): ", hipGetErrorName(err), ": ", hipGetErrorString(err));
+  __builtin_unreachable();
+}
+
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -1426,6 +1439,13 @@ std::vector<at::Tensor> gelu_bwd_bias(const at::Tensor& dg, const at::Tensor& h,
 
 }  // namespace
 
+at::Tensor debug_launch(int64_t n, int64_t mode) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "debug_launch: mode must be 0, 1 or 2");
+  at::Tensor out = at::zeros({n}, at::TensorOptions().device(at::kCUDA).dtype(at::kFloat));
+  damd_debug_launch(out.data_ptr<float>(), static_cast<int>(n), static_cast<int>(mode), cur_stream());
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("occupy", [](int64_t nblk, double usec) {  // CU-occupancy probe on the current stream
     static at::Tensor sink;
@@ -1436,6 +1456,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lm_ce_bwd", &lm_ce_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("gelu_fwd", &gelu_fwd);
+  m.def("debug_launch", &debug_launch, "launch-check probe: mode 0 valid, 1 LDS over the limit, 2 oversized block");
   m.def("gelu_bwd_bias", &gelu_bwd_bias);
   m.def("attn_supported", &attn_supported);
   m.def("attn_fwd", &attn_fwd);

@@ -747,26 +747,26 @@ void damd_bn_fwd_launch(const void* x, const void* res, void* y, int64_t M, int 
     nb = pre_nb;
     pilot = nullptr;
   } else if (x_dtype == 1) {
-    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
+    DAMD_LAUNCH(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
   } else {
-    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+    DAMD_LAUNCH(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
   }
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
+    DAMD_LAUNCH(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
+    DAMD_LAUNCH(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
-#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR, nullptr)
+#define APPLY(T, R, A) DAMD_LAUNCH((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR, nullptr)
   if (mask != nullptr && res && relu) {
     if (x_dtype == 1)
-      hipLaunchKernelGGL((bn_apply_kernel<bf16_t, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift, static_cast<const bf16_t*>(res), static_cast<bf16_t*>(y), V, TPR, mask);
+      DAMD_LAUNCH((bn_apply_kernel<bf16_t, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift, static_cast<const bf16_t*>(res), static_cast<bf16_t*>(y), V, TPR, mask);
     else
-      hipLaunchKernelGGL((bn_apply_kernel<float, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift, static_cast<const float*>(res), static_cast<float*>(y), V, TPR, mask);
+      DAMD_LAUNCH((bn_apply_kernel<float, true, true, true>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift, static_cast<const float*>(res), static_cast<float*>(y), V, TPR, mask);
   } else if (x_dtype == 1) {
     if (res) { if (relu) APPLY(bf16_t, true, true); else APPLY(bf16_t, true, false); }
     else { if (relu) APPLY(bf16_t, false, true); else APPLY(bf16_t, false, false); }
@@ -786,11 +786,11 @@ void damd_bn_finalize_launch(const float* part, int nb, int C, int64_t M, const 
                              float* scale, float* shift, int w_dtype, hipStream_t st) {
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
+    DAMD_LAUNCH(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
                        eps, static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd,
                        scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
+    DAMD_LAUNCH(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1, momentum,
                        eps, static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd,
                        scale, shift);
   DAMD_CHECK_LAUNCH();
@@ -801,7 +801,7 @@ void damd_bn_apply_only_launch(const void* x, const void* res, void* y, int64_t 
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
-#define APPLY(T, R, A) hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR)
+#define APPLY(T, R, A) DAMD_LAUNCH((bn_apply_kernel<T, R, A>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(x), scale, shift, static_cast<const T*>(res), static_cast<T*>(y), V, TPR)
   if (x_dtype == 1) {
     if (res) { if (relu) APPLY(bf16_t, true, true); else APPLY(bf16_t, true, false); }
     else { if (relu) APPLY(bf16_t, false, true); else APPLY(bf16_t, false, false); }
@@ -821,9 +821,9 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   const int64_t rpb = rows_per_block_for(M, C, &nb);
   const bool has_res = res != nullptr || mask != nullptr;
   const bool masked = mask != nullptr && relu;
-#define RED(T, R, A) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part, nullptr)
+#define RED(T, R, A) DAMD_LAUNCH((bn_bwd_reduce_kernel<T, R, A>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), mean, scale, shift, M, C, rpb, part, nullptr)
   // a second gradient (dy2) is only taken on the masked residual path (ResNet block outputs)
-#define REDM(T, D2) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true, true, D2>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask, static_cast<const T*>(dy2))
+#define REDM(T, D2) DAMD_LAUNCH((bn_bwd_reduce_kernel<T, true, true, true, D2>), dim3(nb), dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, mean, scale, shift, M, C, rpb, part, mask, static_cast<const T*>(dy2))
   if (masked) {
     if (x_dtype == 1) { if (dy2) REDM(bf16_t, true); else REDM(bf16_t, false); }
     else { if (dy2) REDM(float, true); else REDM(float, false); }
@@ -837,10 +837,10 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
 #undef RED
 #undef REDM
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   if (dx == nullptr) {  // coefficients only: the apply pass is deferred to the consumer (bn_bwd_coef)
     DAMD_CHECK_LAUNCH();
@@ -850,8 +850,8 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
   const bool wd = dres != nullptr;
-#define BAP(T, R, A, W) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, nullptr)
-#define BAPM(T, W, D2) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true, W, true, D2>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, mask, static_cast<const T*>(dy2))
+#define BAP(T, R, A, W) DAMD_LAUNCH((bn_bwd_apply_kernel<T, R, A, W>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(res), scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, nullptr)
+#define BAPM(T, W, D2) DAMD_LAUNCH((bn_bwd_apply_kernel<T, true, true, W, true, D2>), ag, dim3(kBNThreads), 0, st, static_cast<const T*>(dy), static_cast<const T*>(x), nullptr, scale, shift, coef, C, static_cast<T*>(dx), static_cast<T*>(dres), V, TPR, mask, static_cast<const T*>(dy2))
   if (masked) {
     if (x_dtype == 1) {
       if (dy2) { if (wd) BAPM(bf16_t, true, true); else BAPM(bf16_t, false, true); }
@@ -882,10 +882,10 @@ void damd_bn_bwd_launch(const void* dy, const void* x, const void* res, int64_t 
 void damd_bn_bwd_finalize_launch(const float* part, int nb, int C, int64_t M, const float* mean, const float* invstd,
                                  const float* scale, float* coef, void* dgamma, void* dbeta, int w_dtype, hipStream_t st) {
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   DAMD_CHECK_LAUNCH();
 }
@@ -896,10 +896,10 @@ void damd_bn_bwd_apply_coef_launch(const void* dz, const void* x, int64_t M, int
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
   if (x_dtype == 1)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dz),
+    DAMD_LAUNCH((bn_bwd_apply_kernel<bf16_t, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dz),
                        static_cast<const bf16_t*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<bf16_t*>(dx), nullptr, V, TPR);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dz),
+    DAMD_LAUNCH((bn_bwd_apply_kernel<float, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dz),
                        static_cast<const float*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<float*>(dx), nullptr, V, TPR);
   DAMD_CHECK_LAUNCH();
 }
@@ -908,19 +908,19 @@ void damd_bn_bwd_from_part_launch(const void* dz, const void* x, int64_t M, int 
                                   const float* invstd, const float* scale, const float* part, int nb, float* coef,
                                   void* dgamma, void* dbeta, void* dx, int x_dtype, int w_dtype, hipStream_t st) {
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   const int TPR = C / 8;
   const int64_t V = M * C / 8;
   const dim3 ag(apply_grid(V, TPR));
   if (x_dtype == 1)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dz),
+    DAMD_LAUNCH((bn_bwd_apply_kernel<bf16_t, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dz),
                        static_cast<const bf16_t*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<bf16_t*>(dx), nullptr, V, TPR);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dz),
+    DAMD_LAUNCH((bn_bwd_apply_kernel<float, false, false, false>), ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dz),
                        static_cast<const float*>(x), nullptr, nullptr, nullptr, coef, C, static_cast<float*>(dx), nullptr, V, TPR);
   DAMD_CHECK_LAUNCH();
 }
@@ -951,10 +951,10 @@ void damd_hw_broadcast_launch(const void* g, void* out, int64_t N, int64_t HW, i
   const int64_t want = (V + kBNThreads - 1) / kBNThreads;
   const dim3 grid(static_cast<unsigned>(want < 8192 ? want : 8192));
   if (dtype == 1)
-    hipLaunchKernelGGL(hw_broadcast_kernel<bf16_t>, grid, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(g),
+    DAMD_LAUNCH(hw_broadcast_kernel<bf16_t>, grid, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(g),
                        static_cast<bf16_t*>(out), V, TPR, HW, scale);
   else
-    hipLaunchKernelGGL(hw_broadcast_kernel<float>, grid, dim3(kBNThreads), 0, st, static_cast<const float*>(g),
+    DAMD_LAUNCH(hw_broadcast_kernel<float>, grid, dim3(kBNThreads), 0, st, static_cast<const float*>(g),
                        static_cast<float*>(out), V, TPR, HW, scale);
   DAMD_CHECK_LAUNCH();
 }
@@ -974,26 +974,26 @@ void damd_bn_pool_fwd_launch(const void* x, void* y, uint8_t* idx, int64_t N, in
     nb = pre_nb;
     pilot = nullptr;
   } else if (x_dtype == 1) {
-    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
+    DAMD_LAUNCH(bn_stats_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), M, C, rpb, part);
   } else {
-    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
+    DAMD_LAUNCH(bn_stats_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(x), M, C, rpb, part);
   }
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
+    DAMD_LAUNCH(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var, mean, invstd, scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
+    DAMD_LAUNCH(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, rpb, pilot, x_dtype == 1, momentum, eps,
                        static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var, mean, invstd, scale, shift);
   const int TPR = C / 8;
   const int64_t Vout = N * OH * OW * TPR;
   const PoolGeo g{H, W, OH, OW};
   const dim3 ag(apply_grid(Vout, TPR));
   if (x_dtype == 1)
-    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift,
+    DAMD_LAUNCH(bn_relu_maxpool_fwd_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(x), scale, shift,
                        static_cast<bf16_t*>(y), idx, Vout, TPR, g, static_cast<bf16_t*>(xarg));
   else
-    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift,
+    DAMD_LAUNCH(bn_relu_maxpool_fwd_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(x), scale, shift,
                        static_cast<float*>(y), idx, Vout, TPR, g, static_cast<float*>(xarg));
   DAMD_CHECK_LAUNCH();
 }
@@ -1007,16 +1007,16 @@ void damd_stem_pool_bn_fwd_launch(const float* part, int nb, int64_t M, const vo
                                   hipStream_t st) {
   const dim3 fg((C + kFinCh - 1) / kFinCh);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
+    DAMD_LAUNCH(bn_finalize_kernel<bf16_t>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
                        momentum, eps, static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(b), run_mean, run_var,
                        mean, invstd, scale, shift);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
+    DAMD_LAUNCH(bn_finalize_kernel<float>, fg, dim3(kFinThreads), 0, st, part, nb, C, M, int64_t{0}, nullptr, 1,
                        momentum, eps, static_cast<const float*>(w), static_cast<const float*>(b), run_mean, run_var,
                        mean, invstd, scale, shift);
   const int TPR = C / 8;
   const int64_t V = Q * TPR;
-  hipLaunchKernelGGL((bn_apply_kernel<bf16_t, false, true>), dim3(apply_grid(V, TPR)), dim3(kBNThreads), 0, st,
+  DAMD_LAUNCH((bn_apply_kernel<bf16_t, false, true>), dim3(apply_grid(V, TPR)), dim3(kBNThreads), 0, st,
                      static_cast<const bf16_t*>(xarg), scale, shift, nullptr, static_cast<bf16_t*>(y), V, TPR, nullptr);
   DAMD_CHECK_LAUNCH();
 }
@@ -1030,14 +1030,14 @@ void damd_stem_pool_bn_bwd_launch(const void* dp, const void* dp2, const void* x
                                   int w_dtype, hipStream_t st) {
   int nb;
   const int64_t rpb = rows_per_block_for(Q, C, &nb);
-  hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st,
+  DAMD_LAUNCH(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st,
                      static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), static_cast<const bf16_t*>(xarg),
                      mean, scale, shift, Q, C, rpb, part, static_cast<bf16_t*>(dz));
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
                        nb, C, M, mean, invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part,
                        nb, C, M, mean, invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   DAMD_CHECK_LAUNCH();
 }
@@ -1053,31 +1053,31 @@ void damd_bn_pool_bwd_launch(const void* dp, const uint8_t* idx, const void* x, 
   const PoolGeo g{H, W, OH, OW};
   if (xarg != nullptr) {  // pooled-domain reduce (argmax input values saved by the forward)
     if (x_dtype == 1)
-      hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp),
+      DAMD_LAUNCH(pooled_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp),
                          static_cast<const bf16_t*>(dp2), static_cast<const bf16_t*>(xarg), mean, scale, shift, Q, C, rpb, part);
     else
-      hipLaunchKernelGGL(pooled_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp),
+      DAMD_LAUNCH(pooled_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp),
                          static_cast<const float*>(dp2), static_cast<const float*>(xarg), mean, scale, shift, Q, C, rpb, part);
   } else if (x_dtype == 1)
-    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
+    DAMD_LAUNCH(maxpool_bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
                        static_cast<const bf16_t*>(x), mean, scale, shift, Q, C, rpb, part, g);
   else
-    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
+    DAMD_LAUNCH(maxpool_bn_bwd_reduce_kernel<float>, dim3(nb), dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
                        static_cast<const float*>(x), mean, scale, shift, Q, C, rpb, part, g);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<bf16_t>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta), coef);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
+    DAMD_LAUNCH(bn_bwd_finalize_kernel<float>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, part, nb, C, M, mean,
                        invstd, scale, static_cast<float*>(dgamma), static_cast<float*>(dbeta), coef);
   const int TPR = C / 8;
   const int64_t VQ = Q * TPR;
   const dim3 ag(apply_grid(VQ, TPR));
   if (x_dtype == 1)
-    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
+    DAMD_LAUNCH(maxpool_bn_bwd_apply_kernel<bf16_t>, ag, dim3(kBNThreads), 0, st, static_cast<const bf16_t*>(dp), static_cast<const bf16_t*>(dp2), idx,
                        static_cast<const bf16_t*>(x), scale, shift, coef, C, static_cast<bf16_t*>(dx), VQ, TPR, g);
   else
-    hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
+    DAMD_LAUNCH(maxpool_bn_bwd_apply_kernel<float>, ag, dim3(kBNThreads), 0, st, static_cast<const float*>(dp), static_cast<const float*>(dp2), idx,
                        static_cast<const float*>(x), scale, shift, coef, C, static_cast<float*>(dx), VQ, TPR, g);
   DAMD_CHECK_LAUNCH();
 }

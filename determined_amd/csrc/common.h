@@ -94,4 +94,22 @@ __device__ __forceinline__ bool is_aligned16(const void* p) {
 
 }  // namespace damd
 
-#define DAMD_CHECK_LAUNCH() (void)hipGetLastError()
+// Launch checking.  Every kernel launch goes through DAMD_LAUNCH, which reads hipGetLastError() right
+// after the launch; a failure (bad grid, dynamic LDS over the limit, missing code object, ...) raises
+// through launch_failed (defined in the host TU, bindings.cpp) as a C++ exception that the bindings
+// surface as a Python RuntimeError naming the launcher, file and line -- a kernel path never returns
+// an unwritten output tensor silently.
+namespace damd {
+[[noreturn]] void launch_failed(hipError_t err, const char* func, const char* file, int line);
+inline void check_hip(hipError_t err, const char* func, const char* file, int line) {
+  if (err != hipSuccess) launch_failed(err, func, file, line);
+}
+}  // namespace damd
+
+#define DAMD_CHECK(expr) ::damd::check_hip((expr), __func__, __FILE__, __LINE__)
+#define DAMD_CHECK_LAUNCH() DAMD_CHECK(hipGetLastError())
+#define DAMD_LAUNCH(...)          \
+  do {                            \
+    hipLaunchKernelGGL(__VA_ARGS__); \
+    DAMD_CHECK_LAUNCH();          \
+  } while (0)

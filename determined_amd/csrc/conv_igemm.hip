@@ -532,7 +532,10 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
   // r*S + s that fall inside the image.  Per k-step the source is then one 64-bit add of a
   // wave-uniform tap/channel offset and a bit test (the per-k-step im2col arithmetic was ~4
   // VALU instructions per MFMA in the PMC counters).
-  int32_t xbase[NIX];  // bytes (may be negative: only used for taps inside the image)
+  // bytes, modulo 2^32: the tap-(0,0) pixel may lie before the tensor (negative), and inputs are
+  // up to 0xF0000000 bytes, so the offsets are kept unsigned and wrap by definition; for a tap
+  // inside the image xbase + soff is the true (in-range) byte offset
+  uint32_t xbase[NIX];
   uint32_t vmask[NIX];
   const int OHW = g.OH * g.OW;
   auto tile_rows = [&](int pt) __attribute__((always_inline)) {
@@ -544,7 +547,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       const int rem = m - n * OHW;
       const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
       const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
-      xbase[i] = static_cast<int32_t>((((static_cast<int64_t>(n) * g.H + ih0) * g.W + iw0) * g.C + ((slot ^ swz(p)) << 3)) * 2);
+      xbase[i] = static_cast<uint32_t>((((static_cast<int64_t>(n) * g.H + ih0) * g.W + iw0) * g.C + ((slot ^ swz(p)) << 3)) * 2);
       uint32_t bits = 0;
       if (m < g.M) {
         for (int r = 0; r < g.R; ++r) {
@@ -650,7 +653,7 @@ conv_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16
       const int soff = ((l_r * g.W + l_s) * g.C + l_cb * kBK) * 2;  // wave-uniform, bytes
 #pragma unroll
       for (int i = 0; i < NIX; ++i) {
-        const uint32_t off = (vmask[i] >> tap) & 1u ? static_cast<uint32_t>(xbase[i] + soff) : 0xFFFFFFF0u;
+        const uint32_t off = (vmask[i] >> tap) & 1u ? xbase[i] + static_cast<uint32_t>(soff) : 0xFFFFFFF0u;
         dma16b(rs_x, off, 0, sw + (BCO + 8 * (wave + NW * i)) * kBK);
       }
     } else {
@@ -1903,15 +1906,15 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
   do {                                                                                                     \
     if constexpr (NST == 3 && (SC == 0 || SC == 3)) {                                                      \
       if (pro == 1) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 1, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
+        DAMD_LAUNCH((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 1, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
       if (pro == 2) {                                                                                      \
-        hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 2, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
+        DAMD_LAUNCH((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 2, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
         break;                                                                                             \
       }                                                                                                    \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 0, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
+    DAMD_LAUNCH((conv_fwd_kernel<BCO, BP, WCO, NW, NST, E, SC, 0, K_>), grid, dim3(64 * NW), 0, st, xp, wp, yp, part, g, ea, pa, ska); \
   } while (0)
 #define LSK(BCO, BP, WCO, NW, NST, SC, K_)                          \
   do {                                                              \
@@ -1929,8 +1932,8 @@ int damd_conv_fwd_launch(const void* x, const void* w, void* y, float* part, int
 #define H2(BCO, BP, WCO, NW, E, K_, P_)                                                                      \
   do {                                                                                                       \
     auto* kfn = conv3x3_kernel<BCO, BP, WCO, NW, E, K_, P_>;                                                  \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds); \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa);  \
+    DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, hlds)); \
+    DAMD_LAUNCH(kfn, grid, dim3(64 * NW), hlds, st, xp, wp, yp, part, g, ea, HR, ska, pa);  \
   } while (0)
 #define H1(BCO, BP, WCO, NW, E, K_)                        \
   do {                                                     \
@@ -2057,9 +2060,9 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
 #define WG(BCO, BKC, WCO, NST) \
-  hipLaunchKernelGGL((conv_wgrad_kernel<BCO, BKC, WCO, NST>), grid, dim3(kThreads), 0, st, xp, dp, part, g)
+  DAMD_LAUNCH((conv_wgrad_kernel<BCO, BKC, WCO, NST>), grid, dim3(kThreads), 0, st, xp, dp, part, g)
 #define WG8(BCO, BKC, WCO, NST) \
-  hipLaunchKernelGGL((conv_wgrad_kernel<BCO, BKC, WCO, NST, 8>), grid, dim3(512), 0, st, xp, dp, part, g)
+  DAMD_LAUNCH((conv_wgrad_kernel<BCO, BKC, WCO, NST, 8>), grid, dim3(512), 0, st, xp, dp, part, g)
   switch (cfg) {
     case 0: WG(128, 128, 2, 2); break;
     case 1: WG(64, 128, 1, 2); break;
@@ -2079,9 +2082,9 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
   const int64_t n = static_cast<int64_t>(K) * R * S * C;  // multiple of 4 (C % 64 == 0)
   const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)
-    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
   else
-    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
   return 0;
 }
@@ -2136,20 +2139,20 @@ int damd_wgrad3x3_launch(const void* x, const void* dy, float* part, void* dw, i
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
   if (cfg == 0) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<128>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, grid, dim3(512), lds, st, xp, dp, part, g);
+    DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<128>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DAMD_LAUNCH(conv3x3_wgrad_kernel<128>, grid, dim3(512), lds, st, xp, dp, part, g);
   } else {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<64>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, grid, dim3(512), lds, st, xp, dp, part, g);
+    DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_wgrad_kernel<64>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DAMD_LAUNCH(conv3x3_wgrad_kernel<64>, grid, dim3(512), lds, st, xp, dp, part, g);
   }
   const int64_t n = static_cast<int64_t>(K) * 9 * C;
   const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)
-    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
   else
-    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
   return 0;
 }
@@ -2177,16 +2180,16 @@ int damd_conv1x1_bwd_fused_launch(const void* dz, const void* y, const float* co
   constexpr int kK = 256, kC = 64;
   const int lds = ((kK / 64) * 4096 * 3 + 2 * 4096) * 2 + (3 * kK + 3 * kC) * 4;
   auto* kfn = conv1x1_bwd_fused_kernel<kK, kC>;
-  hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(kfn, dim3(G), dim3(512), lds, st, static_cast<const bf16_t*>(dz), static_cast<const bf16_t*>(y),
+  DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  DAMD_LAUNCH(kfn, dim3(G), dim3(512), lds, st, static_cast<const bf16_t*>(dz), static_cast<const bf16_t*>(y),
                      coef, static_cast<const bf16_t*>(wt), static_cast<const bf16_t*>(a), static_cast<const bf16_t*>(yb),
                      bnp, static_cast<int>(M), static_cast<bf16_t*>(dzo), part, wpart);
   const int64_t n = static_cast<int64_t>(K) * C;
   const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
   if (w_dtype == 1)
-    hipLaunchKernelGGL(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, wpart, G, n, static_cast<bf16_t*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, wpart, G, n, static_cast<bf16_t*>(dw));
   else
-    hipLaunchKernelGGL(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, wpart, G, n, static_cast<float*>(dw));
+    DAMD_LAUNCH(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, wpart, G, n, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
   return 0;
 }

@@ -687,7 +687,7 @@ void damd_stem_fwd_launch(const void* x, const void* wk, void* y, float* part, i
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(wk);
   bf16_t* yp = static_cast<bf16_t*>(y);
-#define FWD(T) hipLaunchKernelGGL(stem_conv_fwd_kernel<T>, dim3(grid), dim3(kThreads), 0, st, xp, wp, yp, part, rows, g)
+#define FWD(T) DAMD_LAUNCH(stem_conv_fwd_kernel<T>, dim3(grid), dim3(kThreads), 0, st, xp, wp, yp, part, rows, g)
   switch (g.OW / 16) {
     case 1: FWD(1); break;
     case 2: FWD(2); break;
@@ -715,7 +715,7 @@ void damd_stem_wgrad_launch(const void* x, const void* dy, float* part, void* dw
   const int nb = damd_stem_wgrad_blocks(N, H);
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
-#define WG(S) hipLaunchKernelGGL(stem_conv_wgrad_kernel<S>, dim3(nb), dim3(kThreads), 0, st, xp, dp, part, rows, g)
+#define WG(S) DAMD_LAUNCH(stem_conv_wgrad_kernel<S>, dim3(nb), dim3(kThreads), 0, st, xp, dp, part, rows, g)
   switch ((g.OW + 31) / 32) {
     case 1: WG(1); break;
     case 2: WG(2); break;
@@ -725,9 +725,9 @@ void damd_stem_wgrad_launch(const void* x, const void* dy, float* part, void* dw
 #undef WG
   const dim3 fg(kCo * kPartCols / 64);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(stem_wgrad_finalize_kernel<bf16_t>, fg, dim3(kThreads), 0, st, part, nb, static_cast<bf16_t*>(dw));
+    DAMD_LAUNCH(stem_wgrad_finalize_kernel<bf16_t>, fg, dim3(kThreads), 0, st, part, nb, static_cast<bf16_t*>(dw));
   else
-    hipLaunchKernelGGL(stem_wgrad_finalize_kernel<float>, fg, dim3(kThreads), 0, st, part, nb, static_cast<float*>(dw));
+    DAMD_LAUNCH(stem_wgrad_finalize_kernel<float>, fg, dim3(kThreads), 0, st, part, nb, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
 }
 
@@ -765,7 +765,7 @@ void damd_stem_pool_fwd_launch(const void* x, const void* wk, const void* gamma,
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(wk);
   bf16_t* ap = static_cast<bf16_t*>(xarg);
-#define PF(T) hipLaunchKernelGGL(stem_pool_fwd_kernel<T>, dim3(grid), dim3(kThreads), 0, st, xp, wp, gamma, gamma_bf16, ap, idx, part, items, p)
+#define PF(T) DAMD_LAUNCH(stem_pool_fwd_kernel<T>, dim3(grid), dim3(kThreads), 0, st, xp, wp, gamma, gamma_bf16, ap, idx, part, items, p)
   switch (p.OW / 16) {
     case 1: PF(1); break;
     case 2: PF(2); break;
@@ -789,7 +789,7 @@ void damd_stem_pool_bwd_launch(const void* x, const void* wk, const void* dpz, c
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(wk);
   const bf16_t* dp = static_cast<const bf16_t*>(dpz);
-#define PB(T, S) hipLaunchKernelGGL((stem_pool_bwd_kernel<T, S>), dim3(nb), dim3(kThreads), 0, st, xp, wp, dp, idx, coef, part, items, p)
+#define PB(T, S) DAMD_LAUNCH((stem_pool_bwd_kernel<T, S>), dim3(nb), dim3(kThreads), 0, st, xp, wp, dp, idx, coef, part, items, p)
   switch (p.OW / 16) {
     case 1: PB(1, 1); break;
     case 2: PB(2, 1); break;
@@ -802,9 +802,9 @@ void damd_stem_pool_bwd_launch(const void* x, const void* wk, const void* dpz, c
 #undef PB
   const dim3 fg(kCo * kPartCols / 64);
   if (w_dtype == 1)
-    hipLaunchKernelGGL(stem_wgrad_finalize_kernel<bf16_t>, fg, dim3(kThreads), 0, st, part, nb, static_cast<bf16_t*>(dw));
+    DAMD_LAUNCH(stem_wgrad_finalize_kernel<bf16_t>, fg, dim3(kThreads), 0, st, part, nb, static_cast<bf16_t*>(dw));
   else
-    hipLaunchKernelGGL(stem_wgrad_finalize_kernel<float>, fg, dim3(kThreads), 0, st, part, nb, static_cast<float*>(dw));
+    DAMD_LAUNCH(stem_wgrad_finalize_kernel<float>, fg, dim3(kThreads), 0, st, part, nb, static_cast<float*>(dw));
   DAMD_CHECK_LAUNCH();
 }
 

@@ -242,13 +242,13 @@ extern "C" {
 
 void damd_occupy_launch(int nblk, double usec, int* sink, hipStream_t st) {
   // wall_clock64 runs at 100 MHz on gfx950
-  hipLaunchKernelGGL(occupy_kernel, dim3(nblk), dim3(256), 0, st, static_cast<int64_t>(usec * 100.0), sink);
+  DAMD_LAUNCH(occupy_kernel, dim3(nblk), dim3(256), 0, st, static_cast<int64_t>(usec * 100.0), sink);
 }
 
 void damd_lm_ce_fwd_launch(const void* logits, const int64_t* labels, int64_t rows, int T, int V, int Vp,
                            int64_t ignore_index, float* row_loss, float* lse, hipStream_t st) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(lm_ce_fwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
+  DAMD_LAUNCH(lm_ce_fwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
                      static_cast<const bf16_t*>(logits), labels, T, V, Vp, ignore_index, row_loss, lse);
   DAMD_CHECK_LAUNCH();
 }
@@ -256,7 +256,7 @@ void damd_lm_ce_fwd_launch(const void* logits, const int64_t* labels, int64_t ro
 void damd_lm_ce_bwd_launch(const void* logits, const int64_t* labels, const float* lse, const float* scale,
                            int64_t rows, int T, int V, int Vp, int64_t ignore_index, void* dlogits, hipStream_t st) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(lm_ce_bwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
+  DAMD_LAUNCH(lm_ce_bwd_kernel, dim3(static_cast<unsigned>(rows)), dim3(kCEThreads), 0, st,
                      static_cast<const bf16_t*>(logits), labels, lse, scale, T, V, Vp, ignore_index,
                      static_cast<bf16_t*>(dlogits));
   DAMD_CHECK_LAUNCH();
@@ -281,7 +281,7 @@ void damd_bias_grad_launch(const void* g, int64_t M, int N, int splits, float* p
   if (M <= 0 || N <= 0) return;
   const int64_t rps = (M + splits - 1) / splits;
   dim3 grid((N + kBGCols - 1) / kBGCols, splits);
-  hipLaunchKernelGGL(bias_grad_partial_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g), M, N, rps, part);
+  DAMD_LAUNCH(bias_grad_partial_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g), M, N, rps, part);
   DAMD_CHECK_LAUNCH();
 }
 
@@ -289,7 +289,7 @@ void damd_gelu_fwd_launch(const void* h, void* g, int64_t n, hipStream_t st) {
   const int64_t nvec = n / 8;
   if (nvec <= 0) return;
   const int64_t want = (nvec + 255) / 256;
-  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(static_cast<unsigned>(want < 8192 ? want : 8192)), dim3(256), 0, st,
+  DAMD_LAUNCH(gelu_fwd_kernel, dim3(static_cast<unsigned>(want < 8192 ? want : 8192)), dim3(256), 0, st,
                      static_cast<const bf16_t*>(h), static_cast<bf16_t*>(g), nvec);
   DAMD_CHECK_LAUNCH();
 }
@@ -300,9 +300,29 @@ void damd_gelu_bwd_bias_launch(const void* dg, const void* h, void* dh, int64_t 
   if (M <= 0 || N <= 0) return;
   const int64_t rps = (M + splits - 1) / splits;
   dim3 grid((N + kBGCols - 1) / kBGCols, splits);
-  hipLaunchKernelGGL(gelu_bwd_bias_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(dg),
+  DAMD_LAUNCH(gelu_bwd_bias_kernel, grid, dim3(256), 0, st, static_cast<const bf16_t*>(dg),
                      static_cast<const bf16_t*>(h), static_cast<bf16_t*>(dh), M, N, rps, part);
   DAMD_CHECK_LAUNCH();
 }
 
 }  // extern "C"
+
+// ---- launch-check probe (tests/test_launch_check_gpu.py): fills `out` with 1.0 through a dynamic-LDS
+// round trip; mode 0 = a valid launch, 1 = dynamic LDS far over the 160 KiB per-workgroup limit,
+// 2 = a 2048-thread block (over the 1024-thread limit).  The invalid modes must raise, not return.
+namespace damd {
+__global__ void debug_fill_kernel(float* __restrict__ out, int n) {
+  extern __shared__ float dbg_lds[];
+  dbg_lds[threadIdx.x] = 1.f;
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = dbg_lds[threadIdx.x];
+}
+}  // namespace damd
+
+extern "C" void damd_debug_launch(float* out, int n, int mode, hipStream_t st) {
+  using namespace damd;
+  const int threads = mode == 2 ? 2048 : 256;
+  const size_t lds = mode == 1 ? (size_t{1} << 20) : threads * sizeof(float);
+  DAMD_LAUNCH(debug_fill_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(threads), lds, st, out, n);
+}

@@ -392,7 +392,7 @@ void fwd_dispatch(const void* x, const void* g, const void* b, void* y, float* m
   T* yp = static_cast<T*>(y);
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
   const bool vec_ok = (H % kVecElems) == 0 && nv <= 16;
-#define FWD_NV(N) hipLaunchKernelGGL((norm_fwd_kernel<T, WT, N, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps)
+#define FWD_NV(N) DAMD_LAUNCH((norm_fwd_kernel<T, WT, N, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps)
   if (vec_ok) {
     switch (nv) {
       case 1: FWD_NV(1); break;
@@ -404,7 +404,7 @@ void fwd_dispatch(const void* x, const void* g, const void* b, void* y, float* m
       default: FWD_NV(16); break;
     }
   } else {
-    hipLaunchKernelGGL((norm_fwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps);
+    DAMD_LAUNCH((norm_fwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, xp, gp, bp, yp, mean, rstd, rows, H, eps);
   }
 #undef FWD_NV
   DAMD_CHECK_LAUNCH();
@@ -423,7 +423,7 @@ int bwd_dispatch(const void* dy, const void* x, const float* mean, const float* 
   T* dxp = static_cast<T*>(dx);
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
   const bool vec_ok = (H % kVecElems) == 0 && nv <= 4;  // 5*NV*8 live fp32 regs
-#define BWD_NV(N) hipLaunchKernelGGL((norm_bwd_kernel<T, WT, N, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H)
+#define BWD_NV(N) DAMD_LAUNCH((norm_bwd_kernel<T, WT, N, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H)
   int W = n_blocks;
   if (vec_ok) {
     switch (nv) {
@@ -432,7 +432,7 @@ int bwd_dispatch(const void* dy, const void* x, const float* mean, const float* 
       default: BWD_NV(4); break;
     }
   } else {
-    hipLaunchKernelGGL((norm_bwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H);
+    DAMD_LAUNCH((norm_bwd_generic_kernel<T, WT, RMS>), grid, block, 0, st, dyp, xp, mean, rstd, gp, dxp, part_g, part_b, rows, H);
     W = n_blocks * (kNormThreads / kWave);
   }
 #undef BWD_NV
@@ -475,7 +475,7 @@ void damd_resid_norm_fwd_launch(const void* x, const void* branch, const void* g
   ra.drop_thresh = p > 0.f ? static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0) : 0u;
   const dim3 grid(static_cast<unsigned>((rows + 3) / 4)), block(kNormThreads);
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
-#define RF(T, WT, N) hipLaunchKernelGGL((norm_fwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(x), \
+#define RF(T, WT, N) DAMD_LAUNCH((norm_fwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(x), \
     static_cast<const WT*>(gamma), static_cast<const WT*>(beta), static_cast<T*>(y), mean, rstd, rows, H, eps, ra)
 #define RFN(T, WT) do { switch (nv) { case 1: RF(T, WT, 1); break; case 2: RF(T, WT, 2); break; default: RF(T, WT, 4); } } while (0)
   if (x_dtype == 1 && w_dtype == 1) RFN(bf16_t, bf16_t);
@@ -500,7 +500,7 @@ int damd_resid_norm_bwd_launch(const void* dy, const void* dres_in, const void* 
   const int nb = damd_norm_bwd_blocks(rows);
   const dim3 grid(nb), block(kNormThreads);
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);
-#define RB(T, WT, N) hipLaunchKernelGGL((norm_bwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(dy), \
+#define RB(T, WT, N) DAMD_LAUNCH((norm_bwd_kernel<T, WT, N, false, true>), grid, block, 0, st, static_cast<const T*>(dy), \
     static_cast<const T*>(s), mean, rstd, static_cast<const WT*>(gamma), static_cast<T*>(dx), part_g, part_b, rows, H, rb)
 #define RBN(T, WT) do { switch (nv) { case 1: RB(T, WT, 1); break; case 2: RB(T, WT, 2); break; default: RB(T, WT, 4); } } while (0)
   if (x_dtype == 1 && w_dtype == 1) RBN(bf16_t, bf16_t);
@@ -542,10 +542,10 @@ void damd_norm_wgrad_finalize_launch(const float* part_g, const float* part_b, i
                                      void* dbeta, int w_dtype, hipStream_t st) {
   const dim3 grid((H + 31) / 32, 2);
   if (w_dtype == 1)
-    hipLaunchKernelGGL((wgrad_finalize_kernel<bf16_t>), grid, dim3(256), 0, st, part_g, part_b, W, H,
+    DAMD_LAUNCH((wgrad_finalize_kernel<bf16_t>), grid, dim3(256), 0, st, part_g, part_b, W, H,
                        static_cast<bf16_t*>(dgamma), static_cast<bf16_t*>(dbeta));
   else
-    hipLaunchKernelGGL((wgrad_finalize_kernel<float>), grid, dim3(256), 0, st, part_g, part_b, W, H,
+    DAMD_LAUNCH((wgrad_finalize_kernel<float>), grid, dim3(256), 0, st, part_g, part_b, W, H,
                        static_cast<float*>(dgamma), static_cast<float*>(dbeta));
   DAMD_CHECK_LAUNCH();
 }
@@ -554,6 +554,6 @@ void damd_col_reduce_launch(const float* part, float* out, int W, int H, hipStre
   int S = W / 64;
   if (S < 1) S = 1;
   if (S > 32) S = 32;
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64, S), dim3(256), 0, st, part, out, W, H);
+  DAMD_LAUNCH(col_reduce_kernel, dim3((H + 63) / 64, S), dim3(256), 0, st, part, out, W, H);
   DAMD_CHECK_LAUNCH();
 }

@@ -238,7 +238,7 @@ void damd_adam_launch(const void* chunks, int n_chunks, const GroupHyper& hp, co
                       int g_dtype, int has_lp, hipStream_t stream) {
   if (n_chunks <= 0) return;
   const MTChunk* c = static_cast<const MTChunk*>(chunks);
-#define L_ADAM(...) hipLaunchKernelGGL((adam_kernel<__VA_ARGS__>), dim3(n_chunks), dim3(kOptThreads), 0, stream, c, hp, scale_ptr, found_inf, step_ptr, maximize)
+#define L_ADAM(...) DAMD_LAUNCH((adam_kernel<__VA_ARGS__>), dim3(n_chunks), dim3(kOptThreads), 0, stream, c, hp, scale_ptr, found_inf, step_ptr, maximize)
   if (p_dtype == 0 && g_dtype == 0) { if (has_lp) L_ADAM(float, float, true); else L_ADAM(float, float, false); }
   else if (p_dtype == 0 && g_dtype == 1) { if (has_lp) L_ADAM(float, bf16_t, true); else L_ADAM(float, bf16_t, false); }
   else if (p_dtype == 1 && g_dtype == 1) L_ADAM(bf16_t, bf16_t, false);
@@ -252,7 +252,7 @@ void damd_sgd_launch(const void* chunks, int n_chunks, const GroupHyper& hp, con
                      int g_dtype, int has_lp, int momentum, hipStream_t stream) {
   if (n_chunks <= 0) return;
   const MTChunk* c = static_cast<const MTChunk*>(chunks);
-#define L_SGD(...) hipLaunchKernelGGL((sgd_kernel<__VA_ARGS__>), dim3(n_chunks), dim3(kOptThreads), 0, stream, c, hp, scale_ptr, found_inf, step_ptr, maximize)
+#define L_SGD(...) DAMD_LAUNCH((sgd_kernel<__VA_ARGS__>), dim3(n_chunks), dim3(kOptThreads), 0, stream, c, hp, scale_ptr, found_inf, step_ptr, maximize)
   if (momentum) {
     if (p_dtype == 0 && g_dtype == 0) { if (has_lp) L_SGD(float, float, true, true); else L_SGD(float, float, false, true); }
     else if (p_dtype == 0 && g_dtype == 1) { if (has_lp) L_SGD(float, bf16_t, true, true); else L_SGD(float, bf16_t, false, true); }
@@ -273,22 +273,22 @@ void damd_l2norm_partial_launch(const void* chunks, int n_chunks, float* partial
   if (n_chunks <= 0) return;
   const MTChunk* c = static_cast<const MTChunk*>(chunks);
   if (g_dtype == 0)
-    hipLaunchKernelGGL(l2norm_partial_kernel<float>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, partial);
+    DAMD_LAUNCH(l2norm_partial_kernel<float>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, partial);
   else
-    hipLaunchKernelGGL(l2norm_partial_kernel<bf16_t>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, partial);
+    DAMD_LAUNCH(l2norm_partial_kernel<bf16_t>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, partial);
   DAMD_CHECK_LAUNCH();
 }
 
 void damd_finalize_launch(const float* partial, int n_partial, float inv_loss_scale,
                           const float* inv_scale_ptr, float max_norm, float* out, int32_t* found_inf,
                           float* step_ptr, int check_inf, hipStream_t stream) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, stream, partial, n_partial,
+  DAMD_LAUNCH(finalize_kernel, dim3(1), dim3(1024), 0, stream, partial, n_partial,
                      inv_loss_scale, inv_scale_ptr, max_norm, out, found_inf, step_ptr, check_inf);
   DAMD_CHECK_LAUNCH();
 }
 
 void damd_step_incr_launch(float* step_ptr, const int32_t* found_inf, hipStream_t stream) {
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, stream, step_ptr, found_inf);
+  DAMD_LAUNCH(step_incr_kernel, dim3(1), dim3(1), 0, stream, step_ptr, found_inf);
   DAMD_CHECK_LAUNCH();
 }
 
@@ -297,8 +297,8 @@ void damd_scale_launch(const void* chunks, int n_chunks, const float* scale_ptr,
   if (n_chunks <= 0) return;
   const MTChunk* c = static_cast<const MTChunk*>(chunks);
   if (g_dtype == 0)
-    hipLaunchKernelGGL(scale_kernel<float>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, scale_ptr);
+    DAMD_LAUNCH(scale_kernel<float>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, scale_ptr);
   else
-    hipLaunchKernelGGL(scale_kernel<bf16_t>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, scale_ptr);
+    DAMD_LAUNCH(scale_kernel<bf16_t>, dim3(n_chunks), dim3(kOptThreads), 0, stream, c, scale_ptr);
   DAMD_CHECK_LAUNCH();
 }

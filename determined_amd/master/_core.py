@@ -547,7 +547,8 @@ class Master:
 
     def create_command(self, cmd: List[str], slots: int = 0, env: Optional[Dict[str, str]] = None,
                        kind: str = "COMMAND", workdir_b64: Optional[str] = None,
-                       resource_pool: Optional[str] = None, priority: Optional[int] = None) -> str:
+                       resource_pool: Optional[str] = None, priority: Optional[int] = None,
+                       workspace_id: Optional[int] = None) -> str:
         with self.lock:
             pool = self.check_pool(resource_pool, slots, None)
             task_id = f"{kind.lower()}-{uuid.uuid4().hex[:8]}"
@@ -557,9 +558,13 @@ class Master:
             a.env = env or {}  # type: ignore[attr-defined]
             a.workdir_b64 = workdir_b64  # type: ignore[attr-defined]
             self.allocations[aid] = a
+            owner = self.iam.current() if self.iam is not None else None
             self.db.insert("tasks", id=task_id, type=kind, state="PENDING",
                            config={"cmd": cmd, "slots": slots, "resource_pool": pool,
-                                   "priority": 42 if priority is None else int(priority)},
+                                   "priority": 42 if priority is None else int(priority),
+                                   # who may reach the task's service through the master's proxy
+                                   "owner_id": owner["id"] if owner else None,
+                                   "workspace_id": workspace_id},
                            start_time=time.time())
             self.sched.add_request(aid, task_id, slots, 42 if priority is None else int(priority), 1.0,
                                    self._next_order(), False, pool=pool)
@@ -840,10 +845,13 @@ class Master:
                 # a re-registering agent lists what it still runs: allocations it was given and no
                 # longer knows (its process restarted) are lost, like a lost agent's (reference
                 # test_agent_restart: without container reattach the trial restarts)
+                # ASSIGNED counts too: an agent that pulled a start from its queue and died before
+                # reporting 'started' no longer has it (the agent lists allocations from the moment it
+                # receives their start command)
                 alive = set(running)
                 queued = {c.get("allocation_id") for c in existing.get("queue", []) if c.get("type") == "start"}
                 for a in list(self.allocations.values()):
-                    if a.state == "RUNNING" and a.id not in alive and a.id not in queued and \
+                    if a.state in ("ASSIGNED", "RUNNING") and a.id not in alive and a.id not in queued and \
                             any(x[0] == agent_id for x in a.assignment):
                         logger.warning(f"agent {agent_id} restarted without allocation {a.id}: marking it lost")
                         a.exit_codes[agent_id] = -1
@@ -851,6 +859,19 @@ class Master:
             pool = resource_pool or (existing or {}).get("resource_pool") or self.sched.default_compute
             if pool not in self.sched.pools:
                 raise ValueError(f"resource pool {pool!r} does not exist (pools: {sorted(self.sched.pools)})")
+            if existing is not None and (pool != existing.get("resource_pool") or slots != existing.get("slots")):
+                # moved to another pool / changed its slot count: the scheduler entry is rebuilt, and the
+                # allocations placed through the old entry are lost (their trials restart under
+                # max_restarts in the new layout) instead of being accounted in the wrong pool
+                logger.warning(f"agent {agent_id} re-registered with pool {pool!r} / {slots} slots (was "
+                               f"{existing.get('resource_pool')!r} / {existing.get('slots')}): rebuilding it")
+                for a in list(self.allocations.values()):
+                    if a.state in ("ASSIGNED", "RUNNING") and any(x[0] == agent_id for x in a.assignment):
+                        a.exit_codes[agent_id] = -1
+                        self._finish_allocation(a)
+                existing["queue"] = [c for c in existing.get("queue", []) if c.get("type") != "start"]
+                self.sched.remove_agent(agent_id)
+                self.sched.add_agent(agent_id, slots, pool)
             self.agents[agent_id] = {"id": agent_id, "slots": slots, "host": host, "devices": devices or list(range(slots)),
                                      "gpu": gpu, "label": label, "queue": existing["queue"] if existing else [],
                                      "last_seen": time.time(), "enabled": existing["enabled"] if existing else True,

@@ -486,9 +486,22 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("POST", r"/api/v1/tasks/([^/]+)/proxy")
     def task_proxy(q, b, task_id):
+        """A task registers where its service listens.  Only the cluster identity (the token the
+        master hands to its tasks) or an admin may do so, and only to a loopback address or the host
+        of a registered agent -- never an arbitrary host (the proxy would otherwise be an SSRF path
+        and a way to point another user's notebook at a foreign server)."""
         if m.db.one("SELECT id FROM tasks WHERE id=?", [task_id]) is None:
             raise HTTPError(404, f"task {task_id} not found")
-        m.db.update("tasks", "id", task_id, proxy={k: b.get(k) for k in ("host", "port", "cwd", "env")})
+        if not m.iam.current()["admin"]:
+            raise HTTPError(403, "only the task itself (cluster token) may register its proxy address")
+        host = b.get("host") or "127.0.0.1"
+        agent_hosts = {ag.get("host") for ag in m.agents.values()}
+        if host not in _LOOPBACK and host not in agent_hosts:
+            raise HTTPError(400, f"proxy host {host!r} is neither loopback nor a registered agent's host")
+        port = b.get("port")
+        if port is not None and not (isinstance(port, int) and 0 < port < 65536):
+            raise HTTPError(400, f"invalid proxy port {port!r}")
+        m.db.update("tasks", "id", task_id, proxy={"host": host, "port": port, "cwd": b.get("cwd"), "env": b.get("env")})
         return {}
 
     add_ntsc_routes(route, m)
@@ -781,6 +794,27 @@ def build_routes(m: Master) -> List[Route]:
     return routes
 
 
+_LOOPBACK = frozenset(("127.0.0.1", "localhost", "::1"))
+
+
+def _may_use_proxy(iam: Any, task_cfg: Dict[str, Any]) -> bool:
+    """Reference ``processProxyAuthentication`` (CanGetNSC / CanGetTensorboard): the owner and admins
+    always; in rbac mode also users with view permission on the task's workspace."""
+    if iam is None or iam.mode == "none":
+        return True
+    u = iam.current()
+    if u["admin"] or (task_cfg.get("owner_id") is not None and task_cfg.get("owner_id") == u["id"]):
+        return True
+    return iam.mode == "rbac" and iam.can("view", task_cfg.get("workspace_id"), None, user=u) and \
+        task_cfg.get("workspace_id") is not None
+
+
+def _strip_auth_cookie(cookie: str) -> str:
+    """The master's own session cookie never reaches the proxied service."""
+    kept = [c.strip() for c in cookie.split(";") if c.strip() and c.strip().partition("=")[0] != "auth"]
+    return "; ".join(kept)
+
+
 class _Raw:
     def __init__(self, body: str, ctype: str) -> None:
         self.body = body
@@ -814,13 +848,18 @@ class _Handler(BaseHTTPRequestHandler):
                         if k == "auth":
                             auth = f"Bearer {v}"
                 iam.set_current(iam.authenticate(auth))
-            row = self.master.db.one("SELECT proxy FROM tasks WHERE id=?", [task_id]) if self.master else None
-            px = (row or {}).get("proxy")
+            row = self.master.db.one("SELECT proxy, config FROM tasks WHERE id=?", [task_id]) if self.master else None
+            if row is None or not _may_use_proxy(iam, row.get("config") or {}):
+                raise HTTPError(404, f"task {task_id} not found")  # no existence leak to other users
+            px = row.get("proxy")
             if not px or not px.get("port"):
                 raise HTTPError(404, f"task {task_id} has no proxied service (yet)")
             conn = http.client.HTTPConnection(px.get("host") or "127.0.0.1", int(px["port"]), timeout=60)
             hdrs = {k: v for k, v in self.headers.items() if k.lower() not in ("host", "authorization", "content-length",
-                                                                             "connection")}
+                                                                             "connection", "cookie")}
+            cookie = _strip_auth_cookie(self.headers.get("Cookie") or "")
+            if cookie:
+                hdrs["Cookie"] = cookie
             conn.request(method, rest + (f"?{parsed.query}" if parsed.query else ""), body=raw or None, headers=hdrs)
             resp = conn.getresponse()
             data = resp.read()

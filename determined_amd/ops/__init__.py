@@ -69,6 +69,17 @@ def fusion_enabled(name: str) -> bool:
     return name not in _DISABLED
 
 
+def conv_sk_timeouts(device=None) -> int:
+    """Number of stream-K hand-off time-outs on ``device`` since the last check (resets the counter and
+    the flag buffers; syncs the device).  0 without the extension or a GPU."""
+    import torch
+
+    if _ext is None or not torch.cuda.is_available():
+        return 0
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    return int(_ext.conv_sk_timeouts(torch.empty(0, device=dev), True))
+
+
 def conv_health_check(device=None) -> None:
     """Raise if any stream-K convolution on ``device`` timed out waiting for a partial tile
     (conv_igemm.hip sk_gather: such a tile is written as NaN, never silently wrong).  Syncs the
@@ -79,7 +90,7 @@ def conv_health_check(device=None) -> None:
     if _ext is None or not torch.cuda.is_available():
         return
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    n = int(_ext.conv_sk_timeouts(torch.empty(0, device=dev), True))
+    n = conv_sk_timeouts(dev)
     if n:
         from determined_amd.ops import conv as _conv
 
@@ -101,6 +112,7 @@ from determined_amd.ops.bn import BatchNormAct2d  # noqa: E402
 __all__ = [
     "available",
     "conv_health_check",
+    "conv_sk_timeouts",
     "ext",
     "FusedAdamW",
     "FusedSGD",

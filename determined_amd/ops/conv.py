@@ -313,11 +313,28 @@ def _pick(key: tuple, cands: Dict[object, Callable[[], object]], default) -> obj
     if not _TUNE_ON or len(cands) <= 1 or torch.cuda.is_current_stream_capturing():
         choice = default if default in cands else next(iter(cands))
     else:
-        times = {c: _time_once(fn) for c, fn in cands.items()}
-        times = dict(zip(times, _agreed(list(times.values()))))
+        times = {}
+        for c, fn in cands.items():
+            try:
+                times[c] = _time_once(fn)
+            except RuntimeError as err:  # a checked launch refused this config (DAMD_LAUNCH): not a candidate
+                if "kernel launch failed" not in str(err):
+                    raise
+                times[c] = float("inf")
+        has_sk = any(isinstance(c, int) and ops.ext().conv_sk_cfg(c) for c in cands)
+        # one collective per layer carries the candidate times AND the stream-K time-out count, so
+        # every rank sees a time-out on any rank and all of them exclude stream-K (and raise) together
+        # instead of one rank raising while the others block in the next collective
+        n_to = float(ops.conv_sk_timeouts()) if has_sk else 0.0
+        agreed = _agreed(list(times.values()) + [n_to])
+        times = dict(zip(times, agreed[:-1]))
+        if agreed[-1] > 0:
+            exclude_stream_k()
+            raise RuntimeError(f"stream-K convolution hand-off(s) timed out while tuning {key} (on some rank): the "
+                               "affected output tiles were written as NaN; stream-K configs are now excluded")
         choice = min(times, key=times.get)
-        if any(isinstance(c, int) and ops.ext().conv_sk_cfg(c) for c in cands):
-            ops.conv_health_check()  # every candidate ran several times: a hand-off time-out shows here
+        if times[choice] == float("inf"):
+            raise RuntimeError(f"no convolution config for {key} launched successfully")
     _TUNE[key] = choice
     return choice
 

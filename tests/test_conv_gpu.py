@@ -176,3 +176,25 @@ def test_stride2_3x3_dgrad_by_phases(ext, shape):
         dx = C._dgrad_s2_phases(ext, dy, w, (n, cin, hw, hw), c)
         err = ((dx.float() - ref).norm() / ref.norm()).item()
         assert err < 1e-2, (c, err)
+
+
+@pytest.mark.parametrize("k,st", [(3, 2), (1, 2)])
+def test_conv_fwd_input_over_2gib(ext, k, st):
+    """inputs above 2^31 bytes (the batch-2048 default has several) -- the kernel's im2col
+    byte offsets are unsigned 32-bit; images past the 2 GiB mark (and the padded borders, whose tap
+    offsets lie before the tensor) are compared with a chunked fp32 reference."""
+    n, cin, cout, hw = 1400, 256, 64, 56  # 2.25 GB of bf16 input
+    pad = k // 2
+    torch.manual_seed(0)
+    x = torch.empty(n, hw, hw, cin, device="cuda", dtype=torch.bfloat16).normal_().permute(0, 3, 1, 2)
+    assert x.is_contiguous(memory_format=torch.channels_last) and x.numel() * 2 > 2 ** 31
+    w = cl((torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).to(torch.bfloat16))
+    cfgs = [c for c in range(ext.conv_num_cfgs()) if ext.conv_supported(x, w, c, st, pad)]
+    assert cfgs
+    for cfg in cfgs[:3]:
+        y, _ = ext.conv_fwd(x, w, st, pad, False, cfg, 0)
+        for lo in (0, 1330, n - 8):  # before, across and after the 2^31-byte mark
+            ref = F.conv2d(x[lo:lo + 8].float(), w.float(), stride=st, padding=pad)
+            torch.testing.assert_close(y[lo:lo + 8].float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        del y
+    torch.cuda.empty_cache()

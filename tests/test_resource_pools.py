@@ -160,3 +160,46 @@ def test_agent_restart_marks_lost_allocations(pooled):
     s.post("/api/v1/agents/register", {"agent_id": "n", "slots": 8, "resource_pool": "train", "running": [a2.id]})
     assert a1.state == "TERMINATED" and a2.state == "RUNNING"
     assert s.get(f"/api/v1/tasks/{t1}")["task"]["exit_code"] == -1
+
+
+def test_agent_restart_loses_assigned_allocations_too(pooled):
+    """an agent that pulled a start command and died before reporting 'started' (the
+    allocation is ASSIGNED, no longer queued) has that allocation failed on re-registration; one
+    still queued for it, or listed by the agent, is kept."""
+    srv, s = pooled
+    m = srv.master
+    s.post("/api/v1/agents/register", {"agent_id": "n2", "slots": 8, "resource_pool": "train"})
+    t1 = s.post("/api/v1/commands", {"command": ["sleep", "60"], "slots": 1})["task_id"]
+    with m.lock:
+        m._schedule()
+    a1 = next(a for a in m.allocations.values() if a.task_id == t1)
+    assert a1.state == "ASSIGNED"
+    # the agent listing it as running (its start command just arrived) keeps it
+    assert len(s.get("/api/v1/agents/n2/work", params={"timeout_seconds": 0})["commands"]) == 1
+    s.post("/api/v1/agents/register", {"agent_id": "n2", "slots": 8, "resource_pool": "train", "running": [a1.id]})
+    assert a1.state == "ASSIGNED"
+    # a restarted agent (empty list) lost it
+    s.post("/api/v1/agents/register", {"agent_id": "n2", "slots": 8, "resource_pool": "train", "running": []})
+    assert a1.state == "TERMINATED"
+    assert s.get(f"/api/v1/tasks/{t1}")["task"]["exit_code"] == -1
+
+
+def test_agent_reregistering_into_another_pool_moves_its_slots(pooled):
+    """a known agent re-registering with another --resource-pool (or slot count) is
+    rebuilt in the scheduler: its slots count in the new pool, work lands there, and allocations it
+    held through the old pool are failed as lost."""
+    srv, s = pooled
+    m = srv.master
+    s.post("/api/v1/agents/register", {"agent_id": "mv", "slots": 4, "resource_pool": "train"})
+    t1 = s.post("/api/v1/commands", {"command": ["sleep", "60"], "slots": 1, "resource_pool": "train"})["task_id"]
+    assert _assigned(m, t1) == ["mv"]
+    a1 = next(a for a in m.allocations.values() if a.task_id == t1)
+    s.post("/api/v1/agents/register", {"agent_id": "mv", "slots": 2, "resource_pool": "aux", "running": [a1.id]})
+    assert a1.state == "TERMINATED"
+    pools = {p["name"]: p for p in s.get("/api/v1/resource-pools")["resource_pools"]}
+    assert pools["train"]["slots_available"] == 0 and pools["aux"]["slots_available"] == 2
+    assert {a["id"]: a["resource_pool"] for a in s.get("/api/v1/agents")["agents"]} == {"mv": "aux"}
+    # new work for the aux pool lands on it; the train pool has nothing left to offer
+    t2 = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 1, "resource_pool": "aux"})["task_id"]
+    t3 = s.post("/api/v1/commands", {"command": ["sleep", "1"], "slots": 1, "resource_pool": "train"})["task_id"]
+    assert _assigned(m, t2) == ["mv"] and _assigned(m, t3) == []
