@@ -20,3 +20,5 @@ from determined_amd.core._preempt import DummyPreemptContext, PreemptContext, Pr
 from determined_amd.core._profiler import DummyProfilerContext, ProfilerContext
 from determined_amd.core._experimental import DummyExperimentalCoreContext, ExperimentalCoreContext
 from determined_amd.core._context import Context, InvalidHP, init, _dummy_init
+from determined_amd.core._tensorboard_mode import TensorboardMode
+from determined_amd.core._heartbeat import UnmanagedTrialHeartbeat

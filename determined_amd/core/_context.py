@@ -32,7 +32,8 @@ class Context:
                  preempt: Optional[PreemptContext] = None, train: Optional[TrainContext] = None,
                  searcher: Optional[SearcherContext] = None, info: Any = None,
                  profiler: Optional[ProfilerContext] = None, _log_shipper: Any = None,
-                 _tensorboard_manager: Any = None, experimental: Optional[ExperimentalCoreContext] = None) -> None:
+                 _tensorboard_manager: Any = None, experimental: Optional[ExperimentalCoreContext] = None,
+                 _heartbeat: Any = None) -> None:
         self.checkpoint = checkpoint
         self.distributed = distributed or DummyDistributedContext()
         self.preempt = preempt or DummyPreemptContext(self.distributed)
@@ -43,17 +44,22 @@ class Context:
         self.experimental = experimental or DummyExperimentalCoreContext()
         self._log_shipper = _log_shipper
         self._tensorboard_manager = _tensorboard_manager
+        self._heartbeat = _heartbeat
 
     def start(self) -> None:
         self.preempt.start()
         if self._log_shipper is not None:
             self._log_shipper.start()
+        if self._heartbeat is not None:
+            self._heartbeat.start()
 
     def __enter__(self) -> "Context":
         self.start()
         return self
 
     def close(self, exc_type=None, exc_val=None, exc_tb=None) -> None:
+        if self._heartbeat is not None:
+            self._heartbeat.close(exc_type, exc_val, exc_tb)
         self.preempt.close()
         self.profiler._close()
         self.distributed.close()
@@ -119,11 +125,20 @@ def _dummy_init(*, distributed: Optional[DistributedContext] = None,
 def init(*, distributed: Optional[DistributedContext] = None,
          checkpoint_storage: Optional[Union[str, Dict[str, Any]]] = None,
          preempt_mode: PreemptMode = PreemptMode.WorkersAskChief,
-         tensorboard_mode: Any = None, _info: Any = None, _unmanaged: bool = False) -> Context:
+         tensorboard_mode: Any = None, _info: Any = None, _unmanaged: bool = False,
+         _heartbeat_interval: float = 60.0) -> Context:
     """Build a core.Context; on-cluster it talks to the master, off-cluster it runs locally.
 
     ``_info``/``_unmanaged`` are used by ``experimental.core_v2`` for unmanaged trials: the
-    process runs outside the cluster but reports metrics and checkpoints to the master."""
+    process runs outside the cluster but reports metrics and checkpoints to the master (and, on the
+    chief, its RUNNING / COMPLETED / ERROR state plus periodic heartbeats: ``core/_heartbeat.py``).
+
+    ``tensorboard_mode`` (``TensorboardMode`` or "AUTO" / "MANUAL", default AUTO): in AUTO the chief
+    writes reported metrics as TensorBoard scalars and uploads its TensorBoard directory when the
+    context closes; in MANUAL nothing is written or uploaded automatically."""
+    from determined_amd.core._tensorboard_mode import TensorboardMode
+
+    tb_mode = TensorboardMode.parse(tensorboard_mode)
     info = _info if _info is not None else get_cluster_info()
     if info is None:
         return _dummy_init(distributed=distributed, checkpoint_storage=checkpoint_storage,
@@ -146,7 +161,8 @@ def init(*, distributed: Optional[DistributedContext] = None,
         try:
             from determined_amd.tensorboard import build_manager
 
-            tb, tbd_writer = build_manager(cfg, info, distributed)
+            auto_chief = tb_mode == TensorboardMode.AUTO and distributed.rank == 0
+            tb, tbd_writer = build_manager(cfg, info, distributed, sync_on_close=auto_chief, write_metrics=auto_chief)
         except Exception as e:  # tensorboard is best effort
             logger.debug(f"tensorboard disabled: {e}")
         train = TrainContext(session, info.trial.trial_id, info.trial._trial_run_id, info.trial.experiment_id,
@@ -155,10 +171,14 @@ def init(*, distributed: Optional[DistributedContext] = None,
             checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,
                                            info.trial.trial_id, tb)
             _install_stacktrace_on_sigusr1()
+            from determined_amd.core._heartbeat import UnmanagedTrialHeartbeat
+
+            hb = UnmanagedTrialHeartbeat(session, info.trial.trial_id, _heartbeat_interval) \
+                if distributed.rank == 0 else None
             return Context(checkpoint=checkpoint, distributed=distributed,
                            preempt=DummyPreemptContext(distributed, preempt_mode), train=train,
                            searcher=DummySearcherContext(distributed, 10**9), info=info, _tensorboard_manager=tb,
-                           experimental=ExperimentalCoreContext(session, info.trial.trial_id))
+                           experimental=ExperimentalCoreContext(session, info.trial.trial_id), _heartbeat=hb)
         searcher = SearcherContext(session, distributed, info.trial.trial_id, info.trial._trial_run_id,
                                    info.allocation_id, _parse_searcher_units(cfg))
         checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,

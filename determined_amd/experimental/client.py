@@ -23,6 +23,7 @@ import contextvars
 import enum
 import io
 import json
+import logging
 import os
 import pathlib
 import tarfile
@@ -65,6 +66,8 @@ def _s() -> Session:
     assert _session is not None
     return _session
 
+
+logger = logging.getLogger("determined_amd.client")
 
 class ExperimentState(enum.Enum):
     ACTIVE = "ACTIVE"
@@ -159,13 +162,55 @@ class Checkpoint:
         return storage.build(cfg)
 
     def download(self, path: Optional[str] = None, mode: DownloadMode = DownloadMode.AUTO) -> str:
-        if mode == DownloadMode.MASTER:
-            raise NotImplementedError("master-proxied checkpoint download is not supported; use DIRECT")
+        """Fetch the checkpoint into ``path`` (default ``checkpoints/<uuid>``).  DIRECT reads the checkpoint
+        storage from this machine; MASTER streams a tar.gz through the master (for clients without
+        access to the storage); AUTO tries DIRECT and falls back to MASTER (reference
+        ``checkpoint/_checkpoint.py`` download / ``_download_auto``)."""
         path = path or os.path.join("checkpoints", self.uuid)
-        os.makedirs(path, exist_ok=True)
-        self._storage().download(src=self.uuid, dst=path)
-        self.write_metadata_file(os.path.join(path, "metadata.json"))
+        if not os.path.exists(os.path.join(path, "metadata.json")):
+            if mode == DownloadMode.DIRECT:
+                self._download_direct(path)
+            elif mode == DownloadMode.MASTER:
+                self._download_via_master(path)
+            elif mode == DownloadMode.AUTO:
+                try:
+                    self._download_direct(path)
+                except (OSError, RuntimeError) as e:
+                    if (self._data.get("checkpoint_storage") or {}).get("type") == "azure":
+                        raise
+                    logger.info(f"direct download of checkpoint {self.uuid} failed ({e}); proxying through the master")
+                    try:
+                        self._download_via_master(path)
+                    except Exception as e2:
+                        raise RuntimeError(f"checkpoint {self.uuid}: direct download and download through the "
+                                           f"master both failed ({e}; {e2})") from e2
+            else:
+                raise ValueError(f"unknown download mode {mode}")
+        md = os.path.join(path, "metadata.json")
+        if not os.path.exists(md):
+            self.write_metadata_file(md)
         return path
+
+    def _download_direct(self, path: str) -> None:
+        sm = self._storage()
+        base = getattr(sm, "_base_path", None)
+        if base is not None and not os.path.isdir(os.path.join(str(base), self.uuid)):
+            raise FileNotFoundError(f"checkpoint {self.uuid} not found under {base} on this machine")
+        os.makedirs(path, exist_ok=True)
+        sm.download(src=self.uuid, dst=path)
+
+    def _download_via_master(self, path: str) -> None:
+        import io
+        import tarfile
+
+        url = f"{self._session.master_url}/api/v1/checkpoints/{self.uuid}/download"
+        r = self._session._http.get(url, headers={**self._session._headers(), "Accept": "application/gzip"},
+                                    timeout=self._session.timeout)
+        if r.status_code >= 400:
+            raise RuntimeError(f"master could not serve checkpoint {self.uuid}: {r.status_code} {r.text}")
+        os.makedirs(path, exist_ok=True)
+        with tarfile.open(fileobj=io.BytesIO(r.content), mode="r:gz") as tf:
+            tf.extractall(path, filter="data")
 
     def write_metadata_file(self, path: str) -> None:
         with open(path, "w") as f:

@@ -114,16 +114,19 @@ def _unmanaged_info(session: Session, defaults: DefaultConfig, unmanaged: Unmana
 def init_context(*, defaults: Optional[DefaultConfig] = None, unmanaged: Optional[UnmanagedConfig] = None,
                  master: Optional[str] = None, distributed: Optional[core.DistributedContext] = None,
                  checkpoint_storage: Optional[Union[str, Dict[str, Any]]] = None,
-                 preempt_mode: core.PreemptMode = core.PreemptMode.WorkersAskChief) -> core.Context:
+                 preempt_mode: core.PreemptMode = core.PreemptMode.WorkersAskChief,
+                 tensorboard_mode: Any = None) -> core.Context:
     managed = get_cluster_info()
     if managed is not None and managed.task_type == "TRIAL":
-        return core.init(distributed=distributed, checkpoint_storage=checkpoint_storage, preempt_mode=preempt_mode)
+        return core.init(distributed=distributed, checkpoint_storage=checkpoint_storage, preempt_mode=preempt_mode,
+                         tensorboard_mode=tensorboard_mode)
     if defaults is None:
         raise NotImplementedError("either specify `defaults`, or run as a managed experiment")
     session = Session(master or os.environ.get("DET_MASTER", "http://127.0.0.1:8080"))
     ci = _unmanaged_info(session, defaults, unmanaged or UnmanagedConfig(), distributed, checkpoint_storage)
     ctx = core.init(distributed=distributed, checkpoint_storage=checkpoint_storage, preempt_mode=preempt_mode,
-                    _info=ci, _unmanaged=True)
+                    tensorboard_mode=tensorboard_mode, _info=ci, _unmanaged=True,
+                    _heartbeat_interval=float(os.environ.get("DET_UNMANAGED_HEARTBEAT_S", "60")))
     ctx._unmanaged_session = session  # type: ignore[attr-defined]
     return ctx
 
@@ -152,14 +155,16 @@ def init(**kwargs: Any) -> None:
 
 
 def close(state: str = "COMPLETED") -> None:
+    """Finish the trial.  Unmanaged: the chief's heartbeat reports the final state -- ``state``, or ERROR
+    when the process is exiting on an uncaught exception / a non-zero ``sys.exit`` (``core/_heartbeat.py``)."""
     global _context
     if _context is None:
         return
     ctx, _context = _context, None
     try:
-        sess = getattr(ctx, "_unmanaged_session", None)
-        if sess is not None and ctx.distributed.rank == 0:
-            sess.post(f"/api/v1/unmanaged/trials/{ctx.info.trial.trial_id}/close", {"state": state})
+        hb = getattr(ctx, "_heartbeat", None)
+        if hb is not None:
+            hb.requested_state = state
     finally:
         ctx.__exit__(None, None, None)
         _set_globals(None)

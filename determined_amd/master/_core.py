@@ -73,6 +73,7 @@ class TrialRec:
         self.warm_start: Optional[str] = None
         self.no_retry = False                  # log policy cancel_retries matched
         self.excluded_agents: List[str] = []  # log policy exclude_node matched
+        self.last_activity: Optional[float] = None  # unmanaged trials: last state report / heartbeat
 
     def searcher_state(self) -> Dict[str, Any]:
         return {"ops": self.ops, "close_requested": self.close_requested, "early_exit": self.early_exit}
@@ -191,6 +192,7 @@ class Master:
                 if self._closed:
                     return
                 self._check_agents()
+                self._reap_unmanaged()
                 self._schedule()
                 if time.time() - last_cleanup > 600:
                     last_cleanup = time.time()
@@ -317,6 +319,51 @@ class Master:
             tr = TrialRec(tid, eid, rid, hparams or {}, seed)
             exp.trials[rid] = tr
             return {"trial_id": tid, "latest_checkpoint": None, "steps_completed": 0}
+
+    # an unmanaged trial whose chief stopped sending heartbeats for this long is marked ERROR
+    unmanaged_timeout_s = float(os.environ.get("DET_UNMANAGED_TIMEOUT_S", "600"))
+
+    def unmanaged_trial_report(self, tid: int, state: Optional[str]) -> None:
+        """``PATCH /api/v1/trials/<id>`` from an unmanaged trial's heartbeat: RUNNING on start,
+        bare heartbeats while it runs, COMPLETED / ERROR / CANCELED at the end."""
+        with self.lock:
+            exp, tr = self._trial(tid)
+            if not getattr(exp, "unmanaged", False):
+                raise ValueError(f"trial {tid} is managed by the master: its state is not reported by the trial")
+            tr.last_activity = time.time()
+            if state is None:
+                return
+            state = str(state).upper()
+            if state == "RUNNING":
+                if tr.state in TERMINAL_TRIAL:  # a resumed run
+                    tr.state = "ACTIVE"
+                    self._persist_trial(tr)
+                if exp.state in TERMINAL_EXP:
+                    exp.state = "ACTIVE"
+                    self.db.update("experiments", "id", exp.id, state="ACTIVE", end_time=None)
+                return
+            if state not in TERMINAL_TRIAL:
+                raise ValueError(f"unknown trial state {state!r}")
+            tr.last_activity = None
+        self.close_unmanaged_trial(tid, state)
+
+    def _reap_unmanaged(self) -> None:
+        """Unmanaged trials that reported a heartbeat once and then went silent for longer than
+        ``unmanaged_timeout_s`` (the process was killed, its host died) end in ERROR."""
+        now = time.time()
+        for exp in list(self.experiments.values()):
+            if not getattr(exp, "unmanaged", False):
+                continue
+            for tr in list(exp.trials.values()):
+                if tr.state not in TERMINAL_TRIAL and tr.last_activity is not None and \
+                        now - tr.last_activity > self.unmanaged_timeout_s:
+                    logger.warning(f"unmanaged trial {tr.id}: no heartbeat for {now - tr.last_activity:.0f} s, ERROR")
+                    tr.last_activity = None
+                    tr.state = "ERROR"
+                    self._persist_trial(tr)
+                    if all(t.state in TERMINAL_TRIAL for t in exp.trials.values()):
+                        self._set_exp_state(exp, "ERROR" if all(t.state == "ERROR" for t in exp.trials.values())
+                                            else "COMPLETED")
 
     def close_unmanaged_trial(self, tid: int, state: str = "COMPLETED") -> None:
         with self.lock:

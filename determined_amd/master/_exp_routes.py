@@ -77,6 +77,12 @@ def add_exp_routes(route: Callable[[str, str], Callable], m: Any) -> None:
         if row is None:
             raise HTTPError(404, f"trial {tid} not found")
         _guard_exp(m, row["experiment_id"], "edit")
+        if "state" in b or b.get("heartbeat"):
+            # unmanaged trials report their own state and heartbeats (core/_heartbeat.py)
+            try:
+                m.unmanaged_trial_report(int(tid), b.get("state"))
+            except ValueError as e:
+                raise HTTPError(400, str(e))
         if "log_retention_days" in b:
             # per-trial retention: logs of this trial are dropped once it is older than N days
             v = b["log_retention_days"]

@@ -7,6 +7,7 @@ block on the master's condition variable.
 
 import base64
 import json
+import pathlib
 import logging
 import re
 import threading
@@ -394,6 +395,39 @@ def build_routes(m: Master) -> List[Route]:
             if row.get("experiment_id") else None
         row["checkpoint_storage"] = (exp or {}).get("config", {}).get("checkpoint_storage") if exp else None
         return {"checkpoint": row}
+
+    @route("GET", r"/api/v1/checkpoints/([0-9a-f\-]+)/download")
+    def download_ckpt(q, b, u):
+        """The checkpoint's files as one tar.gz streamed by the master (reference ``DownloadMode.MASTER``,
+        ``GET /checkpoints/<uuid>`` with ``Accept: application/gzip``): for clients that cannot reach the
+        checkpoint storage themselves.  The master reads it through the experiment's storage config."""
+        import io
+        import tarfile
+        import tempfile
+
+        from determined_amd import storage as det_storage
+
+        row = m.db.one("SELECT * FROM checkpoints WHERE uuid=?", [u])
+        if row is None:
+            raise HTTPError(404, f"checkpoint {u} not found")
+        if row.get("state") == "DELETED":
+            raise HTTPError(409, f"checkpoint {u} was deleted")
+        exp = m.db.one("SELECT id, config FROM experiments WHERE id=?", [row["experiment_id"]]) \
+            if row.get("experiment_id") else None
+        if exp is None:
+            raise HTTPError(404, f"checkpoint {u} has no experiment storage configuration")
+        _guard_exp(m, exp["id"], "view")
+        sm = det_storage.build((exp.get("config") or {}).get("checkpoint_storage"))
+        buf = io.BytesIO()
+        with tempfile.TemporaryDirectory() as td:
+            try:
+                sm.download(src=u, dst=td)
+            except (OSError, RuntimeError) as e:
+                raise HTTPError(502, f"master could not read checkpoint {u} from storage: {e}")
+            with tarfile.open(fileobj=buf, mode="w:gz") as tf:
+                for f in sorted(pathlib.Path(td).rglob("*")):
+                    tf.add(str(f), arcname=str(f.relative_to(td)), recursive=False)
+        return _Raw(buf.getvalue(), "application/gzip")
 
     @route("PATCH", r"/api/v1/checkpoints/([0-9a-f\-]+)")
     def patch_ckpt(q, b, u):
@@ -816,7 +850,7 @@ def _strip_auth_cookie(cookie: str) -> str:
 
 
 class _Raw:
-    def __init__(self, body: str, ctype: str) -> None:
+    def __init__(self, body: Any, ctype: str) -> None:  # str or bytes
         self.body = body
         self.ctype = ctype
 
@@ -915,7 +949,7 @@ class _Handler(BaseHTTPRequestHandler):
             else:
                 raise HTTPError(404, f"no route {method} {parsed.path}")
             if isinstance(out, _Raw):
-                data, ctype = out.body.encode(), out.ctype
+                data, ctype = (out.body if isinstance(out.body, bytes) else out.body.encode()), out.ctype
             else:
                 data = json.dumps(out, default=str).encode()
         except (HTTPError, AuthError) as e:

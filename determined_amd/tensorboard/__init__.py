@@ -121,8 +121,10 @@ class MetricWriter:
 
 
 class TensorboardManager:
-    def __init__(self, base_path: pathlib.Path, storage_manager: Any, sync_path: str) -> None:
+    def __init__(self, base_path: pathlib.Path, storage_manager: Any, sync_path: str,
+                 sync_on_close: bool = True) -> None:
         self.base_path = pathlib.Path(base_path)
+        self.sync_on_close = sync_on_close  # TensorboardMode.AUTO on the chief
         self.base_path.mkdir(parents=True, exist_ok=True)
         self._sm = storage_manager
         self._sync_path = sync_path
@@ -153,17 +155,21 @@ class TensorboardManager:
                 shutil.copy2(p, target / rel)
 
     def close(self) -> None:
+        if not self.sync_on_close:
+            return
         try:
             self.sync()
         except Exception:
             pass
 
 
-def build_manager(cfg: Dict[str, Any], info: Any, dist: Any) -> Tuple[TensorboardManager, MetricWriter]:
+def build_manager(cfg: Dict[str, Any], info: Any, dist: Any, sync_on_close: bool = True,
+                  write_metrics: bool = True) -> Tuple[TensorboardManager, Optional[MetricWriter]]:
     from determined_amd import storage
 
     sm = storage.build(cfg.get("tensorboard_storage") or cfg["checkpoint_storage"])
     base = pathlib.Path(os.environ.get("DET_TENSORBOARD_DIR", "/tmp/tensorboard")) / \
         f"exp-{info.trial.experiment_id}-trial-{info.trial.trial_id}"
-    mgr = TensorboardManager(base, sm, f"tensorboard/experiment/{info.trial.experiment_id}/trial/{info.trial.trial_id}")
-    return mgr, MetricWriter(str(base), dist.rank)
+    mgr = TensorboardManager(base, sm, f"tensorboard/experiment/{info.trial.experiment_id}/trial/{info.trial.trial_id}",
+                             sync_on_close=sync_on_close)
+    return mgr, (MetricWriter(str(base), dist.rank) if write_metrics else None)
