@@ -183,11 +183,18 @@ py::dict request_to_py(const Request& r) {
 
 namespace damd_native {
 void register_loader(py::module& m);
-}
+// searcher.cpp (adaptive_asha.go getBracketMaxTrials / getBracketMaxConcurrentTrials), exposed for the
+// Go test vectors in tests/test_searcher_go_vectors.py
+std::vector<int64_t> bracket_max_trials(int64_t max_trials, double divisor, const std::vector<int64_t>& br);
+std::vector<int64_t> bracket_max_concurrent(int64_t mct, double divisor, const std::vector<int64_t>& mt);
+}  // namespace damd_native
 
 PYBIND11_MODULE(_native, m) {
   damd_native::register_loader(m);
   m.doc() = "determined_amd native control plane: search methods + scheduler";
+  m.def("bracket_max_trials", &damd_native::bracket_max_trials, py::arg("max_trials"), py::arg("divisor"), py::arg("rungs"));
+  m.def("bracket_max_concurrent", &damd_native::bracket_max_concurrent, py::arg("max_concurrent_trials"), py::arg("divisor"),
+        py::arg("max_trials"));
   py::class_<SearchEngine>(m, "SearchEngine")
       .def(py::init<const py::dict&, const py::list&, uint64_t>(), py::arg("config"), py::arg("hparams"),
            py::arg("seed"))

@@ -669,7 +669,7 @@ class Tournament : public SearchMethod {
 };
 
 // adaptive_asha.go:getBracketMaxTrials
-static std::vector<int64_t> bracket_max_trials(int64_t max_trials, double divisor, const std::vector<int64_t>& br) {
+std::vector<int64_t> bracket_max_trials(int64_t max_trials, double divisor, const std::vector<int64_t>& br) {
   std::vector<double> w;
   double tot = 0;
   for (auto r : br) {
@@ -687,7 +687,7 @@ static std::vector<int64_t> bracket_max_trials(int64_t max_trials, double diviso
 }
 
 // adaptive_asha.go:getBracketMaxConcurrentTrials
-static std::vector<int64_t> bracket_max_concurrent(int64_t mct, double divisor, const std::vector<int64_t>& mt) {
+std::vector<int64_t> bracket_max_concurrent(int64_t mct, double divisor, const std::vector<int64_t>& mt) {
   const int64_t nb = static_cast<int64_t>(mt.size());
   int64_t min_trials, rem = 0;
   if (mct == 0) {

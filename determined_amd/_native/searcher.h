@@ -75,7 +75,7 @@ struct Operation {
   bool cancel = false, failure = false;  // Shutdown
 };
 
-enum class ExitedReason { Errored = 0, UserCanceled = 1, InvalidHP = 2, InitInvalidHP = 3 };
+enum class ExitedReason { Errored = 0, UserCanceled = 1, InvalidHP = 2, InitInvalidHP = 3, UserRequestedStop = 4 };
 
 struct Context {
   std::mt19937_64* rng;

@@ -1132,7 +1132,7 @@ class Master:
             if tr.early_exit is not None:
                 raise ValueError("early exit already reported")
             tr.early_exit = {"EXITED_REASON_INVALID_HP": "invalid_hp",
-                             "EXITED_REASON_USER_REQUESTED_STOP": "user_canceled"}.get(reason, "errored")
+                             "EXITED_REASON_USER_REQUESTED_STOP": "user_requested_stop"}.get(reason, "errored")
             self._persist_trial(tr)
 
     def preemption_signal(self, alloc_id: str, timeout: float) -> bool:

@@ -27,6 +27,7 @@ class ExitedReason(enum.Enum):
     USER_CANCELED = "user_canceled"
     INVALID_HP = "invalid_hp"
     INIT_INVALID_HP = "init_invalid_hp"
+    USER_REQUESTED_STOP = "user_requested_stop"
 
 
 class SearcherState:

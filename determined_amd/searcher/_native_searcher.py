@@ -9,7 +9,7 @@ from typing import Any, Dict, List, Optional, Set, Tuple
 from determined_amd import config as expconf
 
 _TYPES = {"const": 0, "int": 1, "double": 2, "log": 3, "categorical": 4}
-EXIT_REASONS = {"errored": 0, "user_canceled": 1, "invalid_hp": 2, "init_invalid_hp": 3}
+EXIT_REASONS = {"errored": 0, "user_canceled": 1, "invalid_hp": 2, "init_invalid_hp": 3, "user_requested_stop": 4}
 
 
 def flatten_hparams(hps: Dict[str, Any], prefix: str = "") -> Tuple[List[Dict[str, Any]], Dict[str, List[Any]]]:
@@ -97,7 +97,7 @@ class Searcher:
 
     def trial_exited_early(self, request_id: int, reason: str) -> List[Dict[str, Any]]:
         self.closed.add(request_id)
-        return self._decode(self.engine.trial_exited_early(request_id, EXIT_REASONS[reason]))
+        return self._decode(self.engine.trial_exited_early(request_id, EXIT_REASONS[reason.lower()]))
 
     def set_trial_progress(self, request_id: int, units: float) -> None:
         self.trial_progress[request_id] = float(units)
