@@ -22,7 +22,7 @@ import shlex
 import subprocess
 import sys
 import sysconfig
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 PKG = pathlib.Path(__file__).resolve().parent
 ROOT = PKG.parent
@@ -31,7 +31,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("DAMD_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip", "conv_igemm.hip"]
+HIP_SOURCES = ["optim.hip", "norm.hip", "bn.hip", "attention.hip", "fused.hip", "conv_stem.hip", "conv_igemm.hip", "conv3x3v2.hip"]
 # MFMA kernels whose accumulators are also touched by VALU code (online softmax, rescales):
 # keep them in the unified VGPR file instead of AGPRs, which otherwise costs a
 # v_accvgpr_read/write pair per element per tile (attention: 450 copies per kv tile) and
@@ -124,26 +124,49 @@ def build_hip_ops(force: bool = False, jobs: int = 8) -> pathlib.Path:
     return out
 
 
-def build_native(force: bool = False, jobs: int = 8) -> pathlib.Path:
+SANITIZERS = {"address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+              "thread": ["-fsanitize=thread"]}
+
+
+def sanitizer_runtime(kind: str) -> str:
+    """The gcc runtime to LD_PRELOAD into the (uninstrumented) python that loads a sanitizer build."""
+    lib = {"address": "libasan.so", "thread": "libtsan.so"}[kind]
+
+    def where(name: str) -> str:
+        return subprocess.run([CXX, f"-print-file-name={name}"], stdout=subprocess.PIPE, text=True,
+                              check=True).stdout.strip()
+
+    # libstdc++ preloaded too: python itself does not link it, and the runtime's __cxa_throw interceptor
+    # must find the real symbol at start-up (C++ exceptions thrown by the module otherwise abort)
+    return f"{where(lib)}:{where('libstdc++.so.6')}"
+
+
+def build_native(force: bool = False, jobs: int = 8, sanitize: Optional[str] = None) -> pathlib.Path:
+    """The C++ control plane.  ``sanitize`` ("address" = ASan+UBSan, "thread" = TSan) builds an
+    instrumented copy under build/sanitize-<kind>/ instead of the in-tree module (load it with
+    DAMD_NATIVE_PATH=<path> and LD_PRELOAD=<sanitizer_runtime(kind)>; tests/test_native_sanitizers.py)."""
     import pybind11
 
     src_dir = PKG / "_native"
     srcs = [src_dir / s for s in NATIVE_SOURCES if (src_dir / s).exists()]
     headers = list(src_dir.glob("*.h"))
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir = BUILD if sanitize is None else ROOT / "build" / f"sanitize-{sanitize}"
+    bdir.mkdir(parents=True, exist_ok=True)
     py_inc = sysconfig.get_paths()["include"]
+    opt = ["-O3"] if sanitize is None else ["-O1", "-g", *SANITIZERS[sanitize]]
     objs, jobs_list = [], []
     for s in srcs:
-        o = BUILD / ("native_" + s.name + ".o")
+        o = bdir / ("native_" + s.name + ".o")
         objs.append(o)
         if force or _newer(o, [s] + headers):
-            jobs_list.append([CXX, "-O3", "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
+            jobs_list.append([CXX, *opt, "-fPIC", "-std=c++17", "-Wall", "-pthread", f"-I{pybind11.get_include()}",
                               f"-I{py_inc}", f"-I{src_dir}", "-c", str(s), "-o", str(o)])
     with concurrent.futures.ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, jobs_list))
-    out = native_path()
+    out = native_path() if sanitize is None else bdir / native_path().name
     if objs and (force or jobs_list or _newer(out, objs)):
-        _run([CXX, "-shared", "-pthread", *map(str, objs), "-o", str(out)])
+        _run([CXX, "-shared", "-pthread", *([] if sanitize is None else SANITIZERS[sanitize]), *map(str, objs),
+              "-o", str(out)])
     return out
 
 
@@ -157,7 +180,12 @@ def main(argv: Sequence[str] = ()) -> int:
     p.add_argument("--force", action="store_true")
     p.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
     p.add_argument("--only", choices=["hip", "native"], default=None)
+    p.add_argument("--sanitize", choices=sorted(SANITIZERS), default=None,
+                   help="build an instrumented copy of the native control plane only")
     a = p.parse_args(list(argv))
+    if a.sanitize:
+        print("built", build_native(a.force, a.jobs, sanitize=a.sanitize))
+        return 0
     if a.only in (None, "native"):
         print("built", build_native(a.force, a.jobs))
     if a.only in (None, "hip"):

@@ -88,6 +88,46 @@ extern "C" int damd_conv_pro_supported_w(int, int, int, int, int, int, int, int)
 extern "C" int64_t damd_conv_sk_ws_floats(int, int, int);
 extern "C" int damd_conv_sk_flag_words();
 extern "C" int damd_conv_cfg_is_sk(int);
+// launchers (conv3x3v2.hip): zero-padded-halo 3x3 kernels, exposed as conv configs
+// damd_conv_num_cfgs() .. + damd_v2_num_cfgs() - 1 (same launch contract as damd_conv_fwd_launch)
+extern "C" int damd_v2_num_cfgs();
+extern "C" int damd_v2_supported(int, int, int, int, int, int, int, int, int);
+extern "C" int damd_v2_groups(int, int, int, int);
+extern "C" int damd_v2_launch(const void*, const void*, void*, float*, int, int, int, int, int, int, int, int, int,
+                              int, int, hipStream_t, int, const void*, const void*, const uint8_t*, const float*,
+                              const float*, const float*, int, const void*, const float*, const float*, const float*,
+                              void*, uint8_t*, float*, int*, int, int);
+namespace {
+int conv_num_cfgs_all() { return damd_conv_num_cfgs() + damd_v2_num_cfgs(); }
+bool is_v2(int cfg) { return cfg >= damd_conv_num_cfgs(); }
+int cfg_supported(int C, int K, int R, int S, int stride, int pad, int H, int W, int cfg) {
+  if (cfg < 0 || cfg >= conv_num_cfgs_all()) return 0;
+  return is_v2(cfg) ? damd_v2_supported(C, K, R, S, stride, pad, H, W, cfg - damd_conv_num_cfgs())
+                    : damd_conv_supported(C, K, R, S, stride, pad, W, cfg);
+}
+int cfg_pro_supported(int C, int K, int R, int S, int stride, int pad, int H, int W, int cfg) {
+  if (cfg < 0 || cfg >= conv_num_cfgs_all()) return 0;
+  return is_v2(cfg) ? damd_v2_supported(C, K, R, S, stride, pad, H, W, cfg - damd_conv_num_cfgs())
+                    : damd_conv_pro_supported_w(C, K, R, S, stride, pad, W, cfg);
+}
+int cfg_groups(int64_t M, int K, int W, int cfg, int groups_override, int64_t N, int64_t H) {
+  return is_v2(cfg) ? damd_v2_groups(static_cast<int>(N), static_cast<int>(H), K, cfg - damd_conv_num_cfgs())
+                    : damd_conv_groups(M, K, W, cfg, groups_override);
+}
+int cfg_launch(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K, int R, int S,
+               int stride, int pad, int cfg, int groups, hipStream_t st, int epi, const void* d2, const void* yb,
+               const uint8_t* mask, const float* mean, const float* scale, const float* shift, int pro,
+               const void* p_res, const float* p_scale, const float* p_shift, const float* p_rscale, void* p_aout,
+               uint8_t* p_mout, float* sk_ws, int* sk_flags, int d2hw, int ophase = 0) {
+  if (is_v2(cfg))
+    return damd_v2_launch(x, w, y, part, N, H, W, C, K, R, S, stride, pad, cfg - damd_conv_num_cfgs(), groups, st,
+                          epi, d2, yb, mask, mean, scale, shift, pro, p_res, p_scale, p_shift, p_rscale, p_aout, p_mout,
+                          sk_ws, sk_flags, d2hw, ophase);
+  return damd_conv_fwd_launch(x, w, y, part, N, H, W, C, K, R, S, stride, pad, cfg, groups, st, epi, d2, yb, mask,
+                              mean, scale, shift, pro, p_res, p_scale, p_shift, p_rscale, p_aout, p_mout, sk_ws,
+                              sk_flags, d2hw, ophase);
+}
+}  // namespace
 // launchers (bn.hip)
 int damd_bn_num_blocks(int64_t, int);
 void damd_bn_fwd_launch(const void*, const void*, void*, int64_t, int, const void*, const void*, float*, float*,
@@ -953,9 +993,9 @@ bool conv_supported(const at::Tensor& x, const at::Tensor& w, int64_t cfg, int64
          x.numel() * 2 < 0xF0000000LL &&  // 32-bit buffer offsets in the kernels (conv_igemm.hip)
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
          w.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.size(1) == x.size(1) &&
-         damd_conv_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(w.size(2)),
-                             static_cast<int>(w.size(3)), static_cast<int>(stride), static_cast<int>(pad),
-                             static_cast<int>(x.size(3)), static_cast<int>(cfg));
+         cfg_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(w.size(2)),
+                       static_cast<int>(w.size(3)), static_cast<int>(stride), static_cast<int>(pad),
+                       static_cast<int>(x.size(2)), static_cast<int>(x.size(3)), static_cast<int>(cfg));
 }
 
 // One phase (a, b) of the input gradient of a stride-2, pad-1 3x3 conv (even input size 2*OH x 2*OW):
@@ -972,8 +1012,8 @@ void conv_dgrad_phase(const at::Tensor& dy, const at::Tensor& wsub, at::Tensor& 
   const int64_t N = dy.size(0), K = dy.size(1), H = dy.size(2), W = dy.size(3), C = wsub.size(0);
   TORCH_CHECK(N * 4 * H * W < (int64_t{1} << 31) - 4096, "conv_dgrad_phase: tensor too large");
   auto wl = wsub.contiguous(at::MemoryFormat::ChannelsLast);
-  const int G = damd_conv_groups(N * H * W, static_cast<int>(C), static_cast<int>(W), static_cast<int>(cfg), 0);
-  const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dx.data_ptr(), nullptr, static_cast<int>(N),
+  const int G = cfg_groups(N * H * W, static_cast<int>(C), static_cast<int>(W), static_cast<int>(cfg), 0, N, H);
+  const int rc = cfg_launch(dy.data_ptr(), wl.data_ptr(), dx.data_ptr(), nullptr, static_cast<int>(N),
                                       static_cast<int>(H), static_cast<int>(W), static_cast<int>(K), static_cast<int>(C),
                                       static_cast<int>(wsub.size(2)), static_cast<int>(wsub.size(3)), 1, 0,
                                       static_cast<int>(cfg), G, cur_stream(), 0, nullptr, nullptr, nullptr, nullptr,
@@ -994,11 +1034,11 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   TORCH_CHECK(M < (int64_t{1} << 31) - 4096 && x.numel() < (int64_t{1} << 40), "conv_fwd: tensor too large");
   auto wl = w.contiguous(at::MemoryFormat::ChannelsLast);
   auto y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg),
-                                 static_cast<int>(groups));
+  const int G = cfg_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg),
+                           static_cast<int>(groups), N, H);
   at::Tensor part = want_stats ? at::empty({G, 2, K}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
   const SkWorkspace sk = sk_workspace(x, K, W, cfg);
-  const int rc = damd_conv_fwd_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
+  const int rc = cfg_launch(x.data_ptr(), wl.data_ptr(), y.data_ptr(), want_stats ? part.data_ptr<float>() : nullptr,
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), static_cast<int>(stride),
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), want_stats ? 1 : 0,
@@ -1020,9 +1060,9 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
   const int64_t R = w.size(2), S = w.size(3), pad = (R - 1) / 2;  // 1x1, or 3x3 / pad 1 (halo kernel)
   TORCH_CHECK(R == S && (R == 1 || R == 3) && conv_supported(y, w, cfg, 1, pad), "conv_bnact_fwd: unsupported input");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3), K = w.size(0);
-  TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
-                                        static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(W),
-                                        static_cast<int>(cfg)),
+  TORCH_CHECK(cfg_pro_supported(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
+                                static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(H), static_cast<int>(W),
+                                static_cast<int>(cfg)),
               "conv_bnact_fwd: config has no prologue variant");
   TORCH_CHECK(R == 1 || !(res.has_value() && res->defined()), "conv_bnact_fwd: no residual operand for 3x3 convs");
   TORCH_CHECK(R == 1 || !want_mask, "conv_bnact_fwd: no ReLU mask output for 3x3 convs");
@@ -1051,10 +1091,10 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
   auto z = at::empty({N, K, H, W}, y.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto a = at::empty_like(y);
   auto mask = want_mask ? at::empty({M * C / 8}, y.options().dtype(at::kByte)) : at::empty({0}, y.options().dtype(at::kByte));
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
+  const int G = cfg_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0, N, H);
   auto part = at::empty({G, 2, K}, y.options().dtype(at::kFloat));
   const SkWorkspace sk = sk_workspace(y, K, W, cfg);
-  const int rc = damd_conv_fwd_launch(y.data_ptr(), wl.data_ptr(), z.data_ptr(), part.data_ptr<float>(),
+  const int rc = cfg_launch(y.data_ptr(), wl.data_ptr(), z.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), 1,
@@ -1068,9 +1108,9 @@ std::vector<at::Tensor> conv_bnact_fwd(const at::Tensor& y, const at::Tensor& w,
 bool conv_pro_supported(const at::Tensor& y, const at::Tensor& w, int64_t cfg) {
   const int64_t R = w.dim() == 4 ? w.size(2) : 0, pad = (R - 1) / 2;
   return (R == 1 || R == 3) && w.size(3) == R && conv_supported(y, w, cfg, 1, pad) &&
-         damd_conv_pro_supported_w(static_cast<int>(y.size(1)), static_cast<int>(w.size(0)), static_cast<int>(R),
-                                   static_cast<int>(R), 1, static_cast<int>(pad), static_cast<int>(y.size(3)),
-                                   static_cast<int>(cfg));
+         cfg_pro_supported(static_cast<int>(y.size(1)), static_cast<int>(w.size(0)), static_cast<int>(R),
+                           static_cast<int>(R), 1, static_cast<int>(pad), static_cast<int>(y.size(2)),
+                           static_cast<int>(y.size(3)), static_cast<int>(cfg));
 }
 
 // Stride-1 input gradient dX = conv(dY, wt, pad) (wt = flipped, transposed weights) of a conv
@@ -1116,7 +1156,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
   TORCH_CHECK(M < (int64_t{1} << 31) - 4096, "conv_dgrad_bn: tensor too large");
   auto wl = wt.contiguous(at::MemoryFormat::ChannelsLast);
   auto dz = at::empty_like(yb);
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
+  const int G = cfg_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0, N, H);
   auto part = at::empty({G, 2, K}, dy.options().dtype(at::kFloat));
   // Deferred BN-backward apply (ops/conv.py _LazyBNGrad): with pro_y given, `dy` holds the
   // following BatchNorm's output gradient dz and the conv's real output gradient is
@@ -1133,9 +1173,9 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
                 "conv_dgrad_bn: pro_coef must be float32 [3, C]");
     TORCH_CHECK(pro_y->sizes() == dy.sizes() && pro_y->strides() == dy.strides() &&
                 pro_y->scalar_type() == at::kBFloat16, "conv_dgrad_bn: pro_y must match dy");
-    TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
-                                          static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(W),
-                                          static_cast<int>(cfg)),
+    TORCH_CHECK(cfg_pro_supported(static_cast<int>(C), static_cast<int>(K), static_cast<int>(R),
+                                  static_cast<int>(S), 1, static_cast<int>(pad), static_cast<int>(H), static_cast<int>(W),
+                                  static_cast<int>(cfg)),
                 "conv_dgrad_bn: config has no prologue variant");
     pro = 2;
     p_res = pro_y->data_ptr();
@@ -1146,7 +1186,7 @@ std::vector<at::Tensor> conv_dgrad_bn(const at::Tensor& dy, const at::Tensor& wt
     p_out = dyo.data_ptr();
   }
   const SkWorkspace sk = sk_workspace(dy, K, W, cfg);
-  const int rc = damd_conv_fwd_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
+  const int rc = cfg_launch(dy.data_ptr(), wl.data_ptr(), dz.data_ptr(), part.data_ptr<float>(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                       static_cast<int>(K), static_cast<int>(R), static_cast<int>(S), 1,
                                       static_cast<int>(pad), static_cast<int>(cfg), G, cur_stream(), mp ? 2 : 3, d2p,
@@ -1166,8 +1206,8 @@ std::vector<at::Tensor> conv_fwd_pro2(const at::Tensor& dz, const at::Tensor& wt
   TORCH_CHECK(wt.dim() == 4 && wt.size(2) == 1 && wt.size(3) == 1 && conv_supported(dz, wt, cfg, 1, 0),
               "conv_fwd_pro2: unsupported input / weight / config");
   const int64_t N = dz.size(0), C = dz.size(1), H = dz.size(2), W = dz.size(3), K = wt.size(0);
-  TORCH_CHECK(damd_conv_pro_supported_w(static_cast<int>(C), static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(W),
-                                        static_cast<int>(cfg)), "conv_fwd_pro2: config has no prologue variant");
+  TORCH_CHECK(cfg_pro_supported(static_cast<int>(C), static_cast<int>(K), 1, 1, 1, 0, static_cast<int>(H),
+                                static_cast<int>(W), static_cast<int>(cfg)), "conv_fwd_pro2: config has no prologue variant");
   TORCH_CHECK(y.sizes() == dz.sizes() && y.strides() == dz.strides() && y.scalar_type() == at::kBFloat16,
               "conv_fwd_pro2: y must match dz");
   TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.dim() == 2 && coef.size(0) == 3 && coef.size(1) == C &&
@@ -1177,9 +1217,9 @@ std::vector<at::Tensor> conv_fwd_pro2(const at::Tensor& dz, const at::Tensor& wt
   auto wl = wt.contiguous(at::MemoryFormat::ChannelsLast);
   auto out = at::empty({N, K, H, W}, dz.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dyo = at::empty_like(dz);
-  const int G = damd_conv_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0);
+  const int G = cfg_groups(M, static_cast<int>(K), static_cast<int>(W), static_cast<int>(cfg), 0, N, H);
   const SkWorkspace sk = sk_workspace(dz, K, W, cfg);
-  const int rc = damd_conv_fwd_launch(dz.data_ptr(), wl.data_ptr(), out.data_ptr(), nullptr, static_cast<int>(N),
+  const int rc = cfg_launch(dz.data_ptr(), wl.data_ptr(), out.data_ptr(), nullptr, static_cast<int>(N),
                                       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(K),
                                       1, 1, 1, 0, static_cast<int>(cfg), G, cur_stream(), 0, nullptr, nullptr, nullptr,
                                       nullptr, nullptr, nullptr, 2, y.data_ptr(), coef[0].data_ptr<float>(),
@@ -1482,7 +1522,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("conv_bnact_fwd", &conv_bnact_fwd);
   m.def("conv_pro_supported", &conv_pro_supported);
-  m.def("conv_num_cfgs", &damd_conv_num_cfgs);
+  m.def("conv_num_cfgs", &conv_num_cfgs_all);
   m.def("wgrad3x3_supported", &wgrad3x3_supported);
   m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported);
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);

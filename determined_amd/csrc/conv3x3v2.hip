@@ -1,0 +1,560 @@
+// 3x3 / stride 1 / pad 1 convolution on a zero-padded LDS halo (gfx950 / MI355X): bf16 NHWC activations,
+// [K][3][3][C] weights, fp32 accumulation on v_mfma_f32_16x16x32_bf16.  Forward, and the input gradient
+// as the forward of the flipped, transposed weights; optional BatchNorm prologue (PRO) / epilogue (EPI)
+// fusions with the same contracts as conv_igemm.hip's generic and halo kernels.
+//
+// Why a second 3x3 kernel.  conv_igemm.hip's halo kernel stages the flattened pixel run
+// m0 - W - 1 ... m0 + BP + W of a tile and reads tap (r, s) at row offset r*W + s: a tap that falls
+// outside the image lands on a neighbouring row / image, so every B-fragment read needs a per-pixel
+// tap-validity test and a select, and its XOR-swizzled LDS address depends on (pixel + tap offset) & 7
+// -- about 8 VALU instructions per B read, the kernel was VALU-issue-bound
+// (profiles/conv3x3_pmc_valu_bound_b1024_1gpu.txt).  Here:
+//   * a tile is TR whole image rows of ONE image (TR | H), so the pixel -> halo-slot map of a lane is
+//     the same for every tile and is computed once per launch;
+//   * the halo is a (TR + 2) x (W + 2) grid of slots with the image border as real zero slots, so no
+//     tap ever needs a validity test;
+//   * a slot is 144 bytes (64 channels + 16 pad bytes): 16 consecutive slots at the same 16-byte
+//     chunk hit 16 distinct bank quads (144 * s mod 256 is distinct for s mod 16), so the reads need
+//     no XOR swizzle; with W a template constant every tap / k-half offset is an immediate of the
+//     ds_read, and a B-fragment read costs no VALU instruction at all;
+//   * the lanes beyond TR * W pixels (W = 56 or 28 is 7 * 2^k: the 16-pixel fragments leave 1/8 of
+//     the lanes idle) read slot 0 and are never stored.
+// The halo is register-staged (global_load_dwordx4 -> optional BN transform -> ds_write_b128), loaded
+// at the first tap of a 64-channel unit and written into the other halo buffer at tap 4, so it
+// overlaps the unit's MFMAs; weights stream per tap through a 3-slot LDS ring filled by the buffer
+// LDS-DMA (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
+// Work split: persistent blocks (one per CU, 8 waves), each a contiguous run of tiles, so consecutive
+// tiles of an image -- which share two halo rows -- run back to back on the same CU / XCD L2.
+
+#include <cstdlib>
+
+#include "common.h"
+
+namespace damd {
+namespace c3v2 {
+
+typedef short s8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int kBK = 64;      // channels per unit (one k-step of 64 per tap)
+constexpr int kSlotB = 144;  // bytes per halo slot
+
+constexpr int kEpiNone = 0, kEpiStats = 1, kEpiBnbM = 2, kEpiBnbR = 3;  // conv_igemm.hip EPI modes
+
+__device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ int swz(int row) { return ((row >> 1) ^ (row >> 3)) & 7; }
+// A-operand row of fragment i for fragment row rho (conv_igemm.hip a_row): lane group g ends with 8
+// consecutive output channels, stored as one 16-byte vector
+__device__ __forceinline__ int a_row(int i, int rho) { return 32 * (i >> 1) + 8 * (rho >> 2) + 4 * (i & 1) + (rho & 3); }
+
+// 16 bytes from rsrc + voff (per lane) + soff (wave-uniform) to LDS (buffer_load_dwordx4 ... lds).  Kept out
+// of the kernel's lambdas: an amdgcn builtin called directly inside them makes hipcc drop the host launch
+// stub of the kernel template (declared, never defined: an undefined symbol at load time)
+__device__ __forceinline__ void dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff, void* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, soff, 0, 0);
+}
+
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+struct Geo {
+  int N, H, C, K;
+  int cblk;     // C / 64
+  int ntiles;   // N * H / TR
+  int ctiles;   // K / BCO
+  int groups;   // blocks per co tile (persistent)
+  uint32_t wbytes;
+};
+
+struct EpiArgs {
+  const bf16_t* yb;      // BN input [M][K] (EPI 2, 3)
+  const uint8_t* mask;   // ReLU bit mask [M][K/8] (EPI 2)
+  const float* mean;     // [K]
+  const float* scale;    // [K] (EPI 3)
+  const float* shift;    // [K] (EPI 3)
+};
+
+struct ProArgs {
+  const bf16_t* res;     // PRO 2: y
+  const float* scale;    // PRO 1: folded BN scale; PRO 2: A
+  const float* shift;    // PRO 1: folded BN shift; PRO 2: Cc
+  const float* rscale;   // PRO 2: B
+  bf16_t* aout;          // the transformed operand [M][C] (tile rows only), or null
+};
+
+// TR image rows x W pixels per tile; BCO output channels per block; WCO co-waves x (NW / WCO) pixel waves
+template <int W, int TR, int BCO, int WCO, int NW>
+struct Shape {
+  static constexpr int WP = W + 2;                      // padded row
+  static constexpr int HS = (TR + 2) * WP;              // halo slots
+  static constexpr int HB = (HS * kSlotB + 255) / 256 * 256;  // halo buffer bytes
+  static constexpr int P = TR * W;                      // real pixels per tile
+  static constexpr int PW = NW / WCO;                   // pixel waves
+  static constexpr int PL = (P + 16 * PW - 1) / (16 * PW) * (16 * PW);  // pixel lanes (>= P)
+  static constexpr int TP = PL / PW, TCO = BCO / WCO;
+  static constexpr int FI = TCO / 16, FJ = TP / 16;
+  static constexpr int NT = 64 * NW;
+  static constexpr int NCH = (HS * 8 + NT - 1) / NT;    // halo 16-byte chunks per thread
+  static constexpr int NIW = BCO / (8 * NW);            // weight DMA instructions per wave per tap
+  static constexpr int WSLOT = BCO * kBK * 2;           // bytes per weight ring slot
+  static constexpr int LDS = 2 * HB + 3 * WSLOT + 3 * BCO * 4;
+  static_assert(FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && WCO * PW == NW, "bad tile");
+  static_assert(NCH <= 8, "halo chunks per thread");
+};
+
+template <int W, int TR, int BCO, int WCO, int NW, int EPI, int PRO>
+__global__ void __launch_bounds__(64 * NW, 1)
+conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                 float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
+  using S = Shape<W, TR, BCO, WCO, NW>;
+  constexpr int FI = S::FI, FJ = S::FJ, NT = S::NT, NCH = S::NCH, NIW = S::NIW;
+  constexpr bool SUMS = EPI != kEpiNone;
+  constexpr int LPC = PRO == 2 ? 2 : 1;  // global loads per halo chunk
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* halo = lds;                             // [2][HB]
+  char* wts = lds + 2 * S::HB;                  // [3][BCO][64] bf16, swizzled
+  float* prm = reinterpret_cast<float*>(wts + 3 * S::WSLOT);  // [3][BCO]: mean, scale, shift
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int rho = lane & 15, lg = lane >> 4;
+  const int wco0 = (wave % WCO) * S::TCO, wp0 = (wave / WCO) * S::TP;
+
+  // block -> (co tile, contiguous tile run); remapped ids keep consecutive runs on one XCD
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ct = rid % g.ctiles, grp = rid / g.ctiles;
+  const int t_begin = static_cast<int>(static_cast<int64_t>(grp) * g.ntiles / g.groups);
+  const int t_end = static_cast<int>(static_cast<int64_t>(grp + 1) * g.ntiles / g.groups);
+  const int units = (t_end - t_begin) * g.cblk;
+  const int tiles_per_img = g.H / TR;
+
+  if (EPI >= kEpiBnbM) {
+    for (int t = tid; t < BCO; t += NT) {
+      const int co = ct * BCO + t;
+      prm[t] = ea.mean[co];
+      prm[BCO + t] = EPI == kEpiBnbR ? ea.scale[co] : 0.f;
+      prm[2 * BCO + t] = EPI == kEpiBnbR ? ea.shift[co] : 0.f;
+    }
+  }
+
+  // ---- halo staging roles (tile-invariant): chunk u = tid + NT * i -> slot u / 8, channel chunk u % 8
+  // (= tid % 8 for every i); relative input offset of the slot's pixel from the tile's first pixel
+  const int hc = tid & 7;
+  int32_t hrel[NCH];     // elements (may be negative); only used when the slot is inside the image
+  uint32_t hlds[NCH];    // byte offset of the chunk in a halo buffer
+  uint32_t hmeta[NCH];   // bit 0: chunk exists and is inside the image columns; bits 8..: padded row hr
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int u = tid + NT * i, slot = u >> 3;
+    const int hr = slot / S::WP, wc = slot - (slot / S::WP) * S::WP;
+    const bool ok = u < S::HS * 8 && wc >= 1 && wc <= W;
+    hrel[i] = ((hr - 1) * W + (wc - 1)) * g.C + hc * 8;
+    hlds[i] = static_cast<uint32_t>(slot * kSlotB + hc * 16);
+    hmeta[i] = (ok ? 1u : 0u) | (static_cast<uint32_t>(hr) << 8) | ((u < S::HS * 8 ? 1u : 0u) << 1);
+  }
+  // ---- B-fragment bases: lane's pixel p = wp0 + 16 j + rho -> slot of tap (0, 0) = (p / W) * WP + p % W
+  uint32_t bb[2][FJ];
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int p = wp0 + 16 * j + rho;
+    const int s0 = p < S::P ? (p / W) * S::WP + (p - (p / W) * W) : 0;
+    bb[0][j] = static_cast<uint32_t>(s0 * kSlotB + lg * 16);
+    bb[1][j] = bb[0][j] + S::HB;
+  }
+  // ---- A-fragment (weight) offsets of ring slot 0; slots are immediates
+  const uint32_t wts_b = 2u * S::HB;
+  uint32_t aoff[2][FI];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int row = wco0 + a_row(i, rho);
+      aoff[kk][i] = wts_b + 2u * static_cast<uint32_t>(row * kBK + (((kk * 4 + lg) ^ swz(row)) << 3));
+    }
+  // ---- weight DMA roles: lane -> (row within its 8-row piece, 16-byte chunk)
+  const int prow = lane >> 3, dslot = lane & 7;
+  const int64_t Ktot = 9LL * g.C;
+  uint32_t wvoff[NIW];
+#pragma unroll
+  for (int i = 0; i < NIW; ++i) {
+    const int co = 8 * (wave + NW * i) + prow;
+    wvoff[i] = static_cast<uint32_t>(((static_cast<int64_t>(ct) * BCO + co) * Ktot + ((dslot ^ swz(co)) << 3)) * 2);
+  }
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(w), 0, static_cast<int>(g.wbytes), 0x00020000);
+
+  // unit index -> (tile, channel block); tile -> image n, first row h0
+  auto unit_tile = [&](int u) __attribute__((always_inline)) { return t_begin + u / g.cblk; };
+  auto unit_cb = [&](int u) __attribute__((always_inline)) { return u - (u / g.cblk) * g.cblk; };
+
+  // weight items: item = unit * 9 + tap; DMA into ring slot item % 3
+  auto issue_w = [&](int item, int rslot) __attribute__((always_inline)) {
+    const int u = item / 9, tap = item - (item / 9) * 9;
+    const int cb = unit_cb(u);
+    const int soff = (tap * g.C + cb * kBK) * 2;  // wave-uniform
+    char* dst = wts + rslot * S::WSLOT;
+#pragma unroll
+    for (int i = 0; i < NIW; ++i)
+      dma16b(rs_w, wvoff[i], soff, dst + 8 * (wave + NW * i) * kBK * 2);
+  };
+
+  // ---- register-staged halo of one unit
+  bf16x8 hx[NCH], hy[PRO == 2 ? NCH : 1];
+  int h_tile = 0, h_cb = 0;
+  auto load_halo = [&](int u) __attribute__((always_inline)) {
+    h_tile = unit_tile(u);
+    h_cb = unit_cb(u);
+    const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
+    const int64_t base = (static_cast<int64_t>(n) * g.H + h0) * W * g.C + h_cb * kBK;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int hr = static_cast<int>(hmeta[i] >> 8);
+      const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
+      const int64_t off = ok ? base + hrel[i] : 0;  // clamped: zeroed at the store
+      hx[i] = *reinterpret_cast<const bf16x8*>(x + off);
+      if (PRO == 2) hy[i] = *reinterpret_cast<const bf16x8*>(pa.res + off);
+    }
+  };
+  auto store_halo = [&](int buf) __attribute__((always_inline)) {
+    const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
+    float fs[8], fh[8], fr[8];
+    if (PRO) {
+      const int c0 = h_cb * kBK + hc * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        fs[e] = pa.scale[c0 + e];
+        fh[e] = pa.shift[c0 + e];
+        fr[e] = PRO == 2 ? pa.rscale[c0 + e] : 0.f;
+      }
+    }
+    const int64_t tile_pix0 = (static_cast<int64_t>(n) * g.H + h0) * W;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      if (!(hmeta[i] & 2u)) continue;  // beyond the halo (last round of chunks)
+      const int hr = static_cast<int>(hmeta[i] >> 8);
+      const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
+      bf16x8 o;
+      if (PRO) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = PRO == 2 ? fs[e] * bf2f(hx[i].v[e]) + fr[e] * bf2f(hy[i].v[e]) + fh[e]
+                                   : fmaxf(bf2f(hx[i].v[e]) * fs[e] + fh[e], 0.f);
+          v[e] = ok ? t : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const u16v2_t pk = f2bf2(v[e], v[e + 1]);
+          o.v[e] = pk[0];
+          o.v[e + 1] = pk[1];
+        }
+      } else {
+        o = ok ? hx[i] : bf16x8{};
+      }
+      *reinterpret_cast<bf16x8*>(halo + buf * S::HB + hlds[i]) = o;
+      // the tile's own rows: the transformed operand is an output (weight gradient / BN backward)
+      if (PRO && pa.aout != nullptr && ct == 0 && ok && hr >= 1 && hr <= TR)
+        *reinterpret_cast<bf16x8*>(pa.aout + tile_pix0 * g.C + hrel[i] + h_cb * kBK) = o;
+    }
+  };
+
+  f4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float st_s[FI / 2][8], st_q[FI / 2][8];
+#pragma unroll
+  for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
+
+  // ---- epilogue of one tile: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel p_j
+  auto epilogue = [&](int tile) __attribute__((always_inline)) {
+    const int n = tile / tiles_per_img, h0 = (tile - n * tiles_per_img) * TR;
+    const int64_t m0 = (static_cast<int64_t>(n) * g.H + h0) * W;
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int p = wp0 + 16 * j + rho;
+      const bool okp = p < S::P;
+      const int64_t m = m0 + (okp ? p : 0);
+      bf16x8 yr[FI / 2];
+      uint32_t mb[FI / 2];
+      if (EPI >= kEpiBnbM) {
+#pragma unroll
+        for (int q = 0; q < FI / 2; ++q) {
+          const int64_t off = m * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
+          yr[q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
+          if (EPI == kEpiBnbM) mb[q] = ea.mask[off >> 3];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < FI / 2; ++q) {
+        const int cl = wco0 + 32 * q + 8 * lg;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = acc[2 * q][j][e]; o[4 + e] = acc[2 * q + 1][j][e]; }
+        float yv[8];
+        if (EPI >= kEpiBnbM) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) yv[e] = bf2f(yr[q].v[e]);
+          if (EPI == kEpiBnbM) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (mb[q] >> e) & 1u ? o[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = yv[e] * prm[BCO + cl + e] + prm[2 * BCO + cl + e] > 0.f ? o[e] : 0.f;
+          }
+        }
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const u16v2_t pk = f2bf2(o[e], o[e + 1]);
+          v.v[e] = pk[0];
+          v.v[e + 1] = pk[1];
+        }
+        if (okp) {
+          *reinterpret_cast<bf16x8*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + cl) = v;
+          if (EPI == kEpiStats) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              st_s[q][e] += o[e];
+              st_q[q][e] += o[e] * o[e];
+            }
+          } else if (EPI >= kEpiBnbM) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float f = bf2f(v.v[e]);
+              st_s[q][e] += f;
+              st_q[q][e] += f * (yv[e] - prm[cl + e]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  const char* lds_c = lds;
+  auto ld = [&](uint32_t off) __attribute__((always_inline)) { return *reinterpret_cast<const s8*>(lds_c + off); };
+
+  // ---- prologue: unit 0's halo into buffer 0, weight items 0 and 1 in flight
+  if (units > 0) {
+    load_halo(0);
+    store_halo(0);
+    issue_w(0, 0);
+    issue_w(1, 1);
+  }
+  const int nitems = units * 9;
+
+  // one tap: item it = u * 9 + T (T compile-time: ring slot T % 3 and the tap's row / column shift are
+  // immediates); HB_: halo buffer of unit u (0 / 1, compile-time via the two-unit unroll)
+  auto tap = [&](auto TT, auto BUF, int u, int it) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value;
+    // the weights of item it landed: younger are item it+1's DMA and, at T = 1, the halo loads issued
+    // at T = 0 (after item it+1's DMA was issued at the previous item)
+    if (it + 1 < nitems) {
+      if (T == 1 && u + 1 < units) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW + NCH * LPC) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's halo stores / last reads
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (T == 0 && u + 1 < units) load_halo(u + 1);
+    if (it + 2 < nitems) issue_w(it + 2, (T + 2) % 3);
+    if (T == 4 && u + 1 < units) store_halo(B ^ 1);  // buffer B^1 was last read by unit u-1
+    constexpr uint32_t toff = static_cast<uint32_t>(((T / 3) * S::WP + (T % 3)) * kSlotB);
+    constexpr uint32_t roff = static_cast<uint32_t>((T % 3) * S::WSLOT);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s8 a[FI], b[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) a[i] = ld(aoff[kk][i] + roff);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) b[j] = ld(bb[B][j] + toff + kk * 64);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+  };
+  auto unit_body = [&](auto BUF, int u) __attribute__((always_inline)) {
+    const int it = u * 9;
+    tap(IC<0>{}, BUF, u, it);
+    tap(IC<1>{}, BUF, u, it + 1);
+    tap(IC<2>{}, BUF, u, it + 2);
+    tap(IC<3>{}, BUF, u, it + 3);
+    tap(IC<4>{}, BUF, u, it + 4);
+    tap(IC<5>{}, BUF, u, it + 5);
+    tap(IC<6>{}, BUF, u, it + 6);
+    tap(IC<7>{}, BUF, u, it + 7);
+    tap(IC<8>{}, BUF, u, it + 8);
+    if (unit_cb(u) == g.cblk - 1) epilogue(unit_tile(u));
+  };
+  for (int u = 0; u < units; u += 2) {
+    unit_body(IC<0>{}, u);
+    if (u + 1 < units) unit_body(IC<1>{}, u + 1);
+  }
+
+  if (SUMS) {  // block reduction of the channel sums into part[grp][2][K]
+#pragma unroll
+    for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          st_s[q][e] += __shfl_xor(st_s[q][e], o, 64);
+          st_q[q][e] += __shfl_xor(st_q[q][e], o, 64);
+        }
+    __syncthreads();
+    constexpr int WPW = S::PW;
+    float* red = reinterpret_cast<float*>(lds);  // [WPW][2][BCO]
+    const int wpi = wave / WCO;
+    if (rho == 0) {
+#pragma unroll
+      for (int q = 0; q < FI / 2; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int co = wco0 + 32 * q + 8 * lg + e;
+          red[(wpi * 2) * BCO + co] = st_s[q][e];
+          red[(wpi * 2 + 1) * BCO + co] = st_q[q][e];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * BCO; t += NT) {
+      const int which = t / BCO, co = t - which * BCO;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < WPW; ++k) s += red[(k * 2 + which) * BCO + co];
+      part[(static_cast<int64_t>(grp) * 2 + which) * g.K + static_cast<int64_t>(ct) * BCO + co] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ host
+struct V2Cfg {
+  int W, TR, bco, wco, nw;
+};
+// 0: 56x56 layers (64 channels), 4-row tiles; 1: 28x28 layers (128 channels), 4-row tiles;
+// 2: 14x14 layers, one image per tile (196 of 256 lanes used)
+constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 8}, {28, 4, 128, 2, 8}, {14, 14, 128, 2, 8}};
+constexpr int kNumV2 = sizeof(kV2) / sizeof(kV2[0]);
+
+template <int W, int TR, int BCO, int WCO, int NW>
+int lds_bytes() {
+  return Shape<W, TR, BCO, WCO, NW>::LDS;
+}
+
+int v2_lds(int cfg) {
+  switch (cfg) {
+    case 0: return lds_bytes<56, 4, 64, 1, 8>();
+    case 1: return lds_bytes<28, 4, 128, 2, 8>();
+    default: return lds_bytes<14, 14, 128, 2, 8>();
+  }
+}
+
+}  // namespace c3v2
+}  // namespace damd
+
+using namespace damd;
+using namespace damd::c3v2;
+
+extern "C" {
+
+int damd_v2_num_cfgs() { return kNumV2; }
+
+// pro: the config is asked for with a BN prologue (1 / 2) -- every v2 config has one
+int damd_v2_supported(int C, int K, int R, int S, int stride, int pad, int H, int W, int cfg) {
+  if (cfg < 0 || cfg >= kNumV2) return 0;
+  const V2Cfg c = kV2[cfg];
+  return R == 3 && S == 3 && stride == 1 && pad == 1 && W == c.W && H > 0 && H % c.TR == 0 && C % kBK == 0 &&
+         C > 0 && K % c.bco == 0 && v2_lds(cfg) <= 160 * 1024;
+}
+
+// stats-partial rows (= blocks per co tile) of a launch
+int damd_v2_groups(int N, int H, int K, int cfg) {
+  const V2Cfg c = kV2[cfg];
+  const int ntiles = N * (H / c.TR), ctiles = K / c.bco;
+  int g = (256 + ctiles - 1) / ctiles;
+  if (g > ntiles) g = ntiles;
+  return g < 1 ? 1 : g;
+}
+
+// Same argument contract as damd_conv_fwd_launch (conv_igemm.hip); no stream-K, no residual operand, no
+// output phase, no compact second gradient.
+int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K, int R,
+                   int S, int stride, int pad, int cfg, int groups, hipStream_t st, int epi, const void* d2,
+                   const void* yb, const uint8_t* mask, const float* mean, const float* scale, const float* shift,
+                   int pro, const void* p_res, const float* p_scale, const float* p_shift, const float* p_rscale,
+                   void* p_aout, uint8_t* p_mout, float* sk_ws, int* sk_flags, int d2hw, int ophase) {
+  (void)sk_ws;
+  (void)sk_flags;
+  (void)p_mout;
+  if (!damd_v2_supported(C, K, R, S, stride, pad, H, W, cfg)) return -1;
+  if (d2 != nullptr || d2hw != 0 || ophase != 0) return -6;
+  if (pro < 0 || pro > 2 || (pro && (p_scale == nullptr || p_shift == nullptr)) ||
+      (pro == 2 && (p_res == nullptr || p_rscale == nullptr)) || (pro == 1 && p_res != nullptr))
+    return -4;
+  if (epi < 0 || epi > 3 || (epi != 0 && part == nullptr)) return -3;
+  if (epi >= 2 && (yb == nullptr || mean == nullptr || (epi == 2 && mask == nullptr) ||
+                   (epi == 3 && (scale == nullptr || shift == nullptr))))
+    return -3;
+  const V2Cfg c = kV2[cfg];
+  const int64_t wbytes = 9LL * C * K * 2;
+  if (wbytes >= 0xF0000000LL || static_cast<int64_t>(N) * H * W >= (int64_t{1} << 31) - 4096) return -7;
+  if (groups != damd_v2_groups(N, H, K, cfg)) return -5;
+  Geo g;
+  g.N = N; g.H = H; g.C = C; g.K = K;
+  g.cblk = C / kBK;
+  g.ntiles = N * (H / c.TR);
+  g.ctiles = K / c.bco;
+  g.groups = groups;
+  g.wbytes = static_cast<uint32_t>(wbytes);
+  const EpiArgs ea{static_cast<const bf16_t*>(yb), mask, mean, scale, shift};
+  const ProArgs pa{static_cast<const bf16_t*>(p_res), p_scale, p_shift, p_rscale, static_cast<bf16_t*>(p_aout)};
+  const dim3 grid(static_cast<unsigned>(g.ctiles * groups));
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* wp = static_cast<const bf16_t*>(w);
+  bf16_t* yp = static_cast<bf16_t*>(y);
+  const int lds = v2_lds(cfg);
+#define V2L(W_, TR_, BCO_, WCO_, NW_, E_, P_)                                                                 \
+  do {                                                                                                       \
+    auto* kfn = conv3x3v2_kernel<W_, TR_, BCO_, WCO_, NW_, E_, P_>;                                           \
+    DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    DAMD_LAUNCH(kfn, grid, dim3(64 * NW_), lds, st, xp, wp, yp, part, g, ea, pa);                              \
+  } while (0)
+#define V2E(W_, TR_, BCO_, WCO_, NW_)                                                                         \
+  do {                                                                                                       \
+    if (epi == 0 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiNone, 0);                                     \
+    else if (epi == 1 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiStats, 0);                               \
+    else if (epi == 1 && pro == 1) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiStats, 1);                               \
+    else if (epi == 2 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbM, 0);                                \
+    else if (epi == 3 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbR, 0);                                \
+    else if (epi == 2 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbM, 2);                                \
+    else if (epi == 3 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbR, 2);                                \
+    else return -4;                                                                                          \
+  } while (0)
+  switch (cfg) {
+    case 0: V2E(56, 4, 64, 1, 8); break;
+    case 1: V2E(28, 4, 128, 2, 8); break;
+    default: V2E(14, 14, 128, 2, 8); break;
+  }
+#undef V2E
+#undef V2L
+  return 0;
+}
+
+}  // extern "C"

@@ -584,6 +584,7 @@ class Master:
     def _start_request(self, exp: ExperimentRec, tr: TrialRec, slots: int) -> None:
         aid = f"trial-{tr.id}.{tr.run_id + 1}.{uuid.uuid4().hex[:6]}"
         a = Allocation(aid, f"trial-{tr.id}", slots, exp.id, tr.id)
+        a.progress_at_start = (tr.total_batches, len(tr.ops))  # type: ignore[attr-defined]
         tr.allocation = a
         self.allocations[aid] = a
         prio = exp.config["resources"].get("priority")
@@ -1025,6 +1026,17 @@ class Master:
             ops = self._finish_trial(exp, tr, "CANCELED")
         elif tr.early_exit:
             ops = self._finish_trial(exp, tr, "COMPLETED")
+        elif (ok and not a.preempt and tr.ops and
+              getattr(a, "progress_at_start", None) == (tr.total_batches, len(tr.ops))):
+            # a clean exit that trained nothing and completed no searcher operation, without being
+            # preempted: counted as a failed run (max_restarts) instead of being rescheduled forever
+            tr.restarts += 1
+            max_restarts = int(exp.config.get("max_restarts", 5))
+            logger.warning(f"trial {tr.id} exited cleanly without progress; restart {tr.restarts}/{max_restarts}")
+            if tr.restarts > max_restarts or tr.no_retry:
+                ops = self._finish_trial(exp, tr, "ERROR")
+            elif exp.state == "ACTIVE":
+                self._request_allocation(exp, tr)
         elif ok or (a.preempt and a.ack_preempt):
             if tr.close_requested and not tr.ops:
                 ops = self._finish_trial(exp, tr, "COMPLETED")
