@@ -515,7 +515,8 @@ class KubernetesBackend:
             c = {"name": self.CONTAINER}
             containers.insert(0, c)
         image = ((cfg.get("environment") or {}).get("image") or {})
-        image = image.get("gpu" if gpn else "cpu") if isinstance(image, dict) else image
+        if isinstance(image, dict):  # normalised expconf image map (cpu / cuda / rocm); MI355X pods use rocm
+            image = (image.get("rocm") or image.get("gpu") or image.get("cuda")) if gpn else image.get("cpu")
         c.setdefault("image", image or self.image)
         penv = dict(env)
         penv.update({"DET_CONTAINER_RANK": str(rank), "DET_K8S_NUM_PODS": str(npods),

@@ -178,6 +178,11 @@ def apply_defaults(cfg: Dict[str, Any], seed: Optional[int] = None) -> Dict[str,
         _merge_defaults(s, {**SEARCHER_DEFAULTS[s["name"]], **SEARCHER_COMMON})
     if cfg.get("name") is None:
         cfg["name"] = "Experiment (unnamed)"
+    env = cfg["environment"]
+    if isinstance(env, dict) and isinstance(env.get("image"), (dict, str)):
+        from determined_amd.config import _schema
+
+        env["image"] = _schema.with_defaults(env["image"], "environment-image.json")
     if cfg["reproducibility"].get("experiment_seed") is None:
         import random as _r
 
@@ -326,9 +331,22 @@ def _flat_hparams(hps: Dict[str, Any], prefix: str = "") -> List[Tuple[str, Dict
     return out
 
 
+def sanity_errors(cfg: Dict[str, Any]) -> List[str]:
+    """Structural errors of a user config against the strict expconf schema (config/_schema.py):
+    unknown keys anywhere, wrong types, out-of-range values, malformed unions -- what the reference's
+    sanity validator reports (master/pkg/schemas/expconf, ``additionalProperties: false``)."""
+    from determined_amd.config import _schema
+
+    return _schema.sanity_errors(cfg, "experiment.json")
+
+
 def parse(src: Union[str, pathlib.Path, Dict[str, Any]], seed: Optional[int] = None) -> Dict[str, Any]:
-    """load + apply_defaults + validate; raises InvalidConfig."""
-    cfg = apply_defaults(load(src), seed=seed)
+    """load + strict sanity check + apply_defaults + validate; raises InvalidConfig."""
+    raw = load(src)
+    errs = sanity_errors(raw)
+    if errs:
+        raise InvalidConfig(errs)
+    cfg = apply_defaults(raw, seed=seed)
     errs = validate(cfg)
     if errs:
         raise InvalidConfig(errs)
