@@ -113,7 +113,10 @@ def main() -> int:
     if "tune" in state and not a.no_pretune:  # kernel choices outside the gradient all-reduce (all ranks alike)
         state["tune"]()
         if rank == 0:
-            print(f"[bench] conv kernels tuned ({time.perf_counter() - t_w:.1f}s)", file=sys.stderr, flush=True)
+            from determined_amd.ops.conv import tuning_seconds
+
+            print(f"[bench] conv kernels tuned ({time.perf_counter() - t_w:.1f}s; {tuning_seconds():.1f}s timing "
+                  f"candidates)", file=sys.stderr, flush=True)
     for i in range(a.warmup):
         step_fn()
         if rank == 0:  # progress on stderr (stdout carries only the JSON line)

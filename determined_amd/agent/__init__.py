@@ -4,7 +4,8 @@
 On an MI355X node the agent owns 8 GPU slots (one per GPU, discovered from the KFD topology in
 sysfs -- the agent never initialises HIP itself, so spawning task processes is safe).  By default
 tasks run as process groups with ``HIP_VISIBLE_DEVICES`` set to their slots; an agent can
-instead front a Slurm/PBS partition or a Kubernetes namespace (``agent/backends.py``).
+instead run them in Docker/Podman containers (``agent/container.py``, re-attached after an agent
+restart) or front a Slurm/PBS partition or a Kubernetes namespace (``agent/backends.py``).
 stdout/stderr are shipped to the master line by line; exit codes are reported back.
 """
 
@@ -65,6 +66,8 @@ class Agent:
         self.resource_pool = resource_pool  # None: the master's default compute pool
         self.backend = backend or ProcessBackend()
         self.agent_id = agent_id or socket.gethostname()
+        if getattr(self.backend, "agent_id", None) == "":  # container labels name their agent
+            self.backend.agent_id = self.agent_id
         self.gpus = detect_gpus() if gpus is None else gpus
         self.use_gpu = bool(self.gpus) and slots is None
         self.devices: List[Any] = list(self.gpus) if self.use_gpu else list(range(slots if slots is not None else 1))
@@ -88,7 +91,43 @@ class Agent:
                                                       "running": sorted(set(self.tasks) | self._starting)})
         logger.info(f"agent {self.agent_id} registered {len(self.devices)} {'GPU' if self.use_gpu else 'CPU'} slots")
 
+    def reattach(self) -> None:
+        """Pick up the tasks a previous agent process left running (container backends): they are
+        listed as running when registering, and followed to their exit like freshly launched ones
+        (reference agent/internal/containers/manager.go:143 reattach)."""
+        if not hasattr(self.backend, "reattach"):
+            return
+        for r in self.backend.reattach():
+            aid = r["allocation_id"]
+            if aid in self.tasks:
+                continue
+            t = _Task({"allocation_id": aid, "task_id": r["task_id"]})
+            t.handle = r["handle"]
+            self.tasks[aid] = t
+            logger.info(f"re-attached to allocation {aid}")
+            threading.Thread(target=self._follow, args=(t, r["task_id"], aid), daemon=True).start()
+
+    def _follow(self, t: _Task, task_id: str, aid: str) -> None:
+        code = -1
+        try:
+            self._pump_logs(t, task_id, aid)
+            assert t.handle is not None
+            code = t.handle.wait()
+        except Exception:
+            logger.exception(f"following re-attached task {aid} failed")
+        finally:
+            self._report_exit(aid, code)
+
+    def _report_exit(self, aid: str, code: int) -> None:
+        self.tasks.pop(aid, None)
+        try:
+            self.session.post(f"/api/v1/agents/{self.agent_id}/events",
+                              {"type": "exited", "allocation_id": aid, "exit_code": code})
+        except Exception as e:
+            logger.warning(f"could not report exit of {aid}: {e}")
+
     def run(self) -> None:
+        self.reattach()
         self.register()
         while not self._stop.is_set():
             try:
@@ -176,12 +215,7 @@ class Agent:
             logger.exception(f"task {aid} failed to run")
             self._ship(c["task_id"], aid, [f"agent: task failed to start: {e!r}"])
         finally:
-            self.tasks.pop(aid, None)
-            try:
-                self.session.post(f"/api/v1/agents/{self.agent_id}/events",
-                                  {"type": "exited", "allocation_id": aid, "exit_code": code})
-            except Exception as e:
-                logger.warning(f"could not report exit of {aid}: {e}")
+            self._report_exit(aid, code)
 
     def _pump_logs(self, t: _Task, task_id: str, aid: str) -> None:
         """Ship log lines in batches (<= 200 lines or 0.5 s old); a flusher thread sends a partial

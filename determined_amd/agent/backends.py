@@ -15,6 +15,9 @@ agent's *backend* decides what "start this task on these slots" means:
   directory, kills go through ``scancel`` (``qdel``).  Experiment-config knobs follow the
   reference schema (``slurm.{slots_per_node,gpu_type,sbatch_args}``,
   ``pbs.{slots_per_node,pbsbatch_args}``; ``schemas/expconf/v0/hpc-cluster-*.json``).
+* :class:`~determined_amd.agent.container.ContainerBackend` -- each task in a Docker / Podman
+  container with the experiment's image, bind mounts, devices and capabilities (the reference Go
+  agent's behaviour), re-attached after an agent restart.
 * :class:`KubernetesBackend` -- one pod per ``slots_per_pod`` GPUs (``amd.com/gpu`` resource)
   created through the Kubernetes REST API; the experiment's ``environment.pod_spec`` is the pod
   template (reference ``kubernetesrm/spec.go``); pods find each other through the master's
@@ -562,4 +565,8 @@ def make_backend(kind: str, **kw: Any):
     if kind == "kubernetes":
         client = KubernetesClient(kw.pop("api_url", None), kw.pop("token", None), kw.pop("verify", None))
         return KubernetesBackend(client, **kw)
+    if kind in ("docker", "podman"):
+        from determined_amd.agent.container import ContainerBackend
+
+        return ContainerBackend(runtime=kind, **kw)
     raise ValueError(f"unknown agent backend {kind!r}")

@@ -183,6 +183,10 @@ def apply_defaults(cfg: Dict[str, Any], seed: Optional[int] = None) -> Dict[str,
         from determined_amd.config import _schema
 
         env["image"] = _schema.with_defaults(env["image"], "environment-image.json")
+    if isinstance(cfg.get("bind_mounts"), list):
+        from determined_amd.config import _schema
+
+        cfg["bind_mounts"] = _schema.with_defaults(cfg["bind_mounts"], "bind-mounts.json")
     if cfg["reproducibility"].get("experiment_seed") is None:
         import random as _r
 

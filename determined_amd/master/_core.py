@@ -596,7 +596,9 @@ class Master:
     def create_command(self, cmd: List[str], slots: int = 0, env: Optional[Dict[str, str]] = None,
                        kind: str = "COMMAND", workdir_b64: Optional[str] = None,
                        resource_pool: Optional[str] = None, priority: Optional[int] = None,
-                       workspace_id: Optional[int] = None) -> str:
+                       workspace_id: Optional[int] = None, task_config: Optional[Dict[str, Any]] = None) -> str:
+        """``task_config``: the expconf sections a command's container honours (environment,
+        bind_mounts, resources) -- shipped to the agent as DET_TASK_CONFIG."""
         with self.lock:
             pool = self.check_pool(resource_pool, slots, None)
             task_id = f"{kind.lower()}-{uuid.uuid4().hex[:8]}"
@@ -605,6 +607,7 @@ class Master:
             a.command = cmd  # type: ignore[attr-defined]
             a.env = env or {}  # type: ignore[attr-defined]
             a.workdir_b64 = workdir_b64  # type: ignore[attr-defined]
+            a.task_config = task_config or None  # type: ignore[attr-defined]
             self.allocations[aid] = a
             owner = self.iam.current() if self.iam is not None else None
             self.db.insert("tasks", id=task_id, type=kind, state="PENDING",
@@ -801,6 +804,7 @@ class Master:
             last = prev[-1] if prev else None
             a.command = cfg.get("cmd")  # type: ignore[attr-defined]
             a.env = getattr(last, "env", {}) if last is not None else {}  # type: ignore[attr-defined]
+            a.task_config = getattr(last, "task_config", None) if last is not None else None  # type: ignore
             a.workdir_b64 = getattr(last, "workdir_b64", None) if last is not None else None  # type: ignore[attr-defined]
             self.allocations[aid] = a
             self.db.update("tasks", "id", task_id, state="PENDING", end_time=None, exit_code=None)
@@ -879,6 +883,8 @@ class Master:
             else:
                 cmd.update(command=getattr(a, "command", []), workdir_b64=getattr(a, "workdir_b64", None))
                 env.update(getattr(a, "env", {}))
+                if getattr(a, "task_config", None):
+                    env["DET_TASK_CONFIG"] = json.dumps(a.task_config)
                 self.db.update("tasks", "id", a.task_id, state="RUNNING")
             ag["queue"].append(cmd)
         self.cv.notify_all()

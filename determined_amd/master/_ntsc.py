@@ -12,7 +12,7 @@ import logging
 import secrets
 import sys
 import time
-from typing import Any, Callable, Deque, Dict, List
+from typing import Any, Callable, Deque, Dict, List, Optional
 
 KINDS = {"notebooks": "NOTEBOOK", "shells": "SHELL", "tensorboards": "TENSORBOARD", "commands": "COMMAND"}
 
@@ -33,6 +33,21 @@ class _RingHandler(logging.Handler):
 
 _RING = _RingHandler()
 logging.getLogger("determined_amd").addHandler(_RING)
+
+
+# the expconf sections a command / notebook / shell / tensorboard container honours (reference
+# CommandConfig: environment, bind_mounts, resources; master/pkg/model/command_config.go)
+TASK_CONFIG_KEYS = ("environment", "bind_mounts", "resources")
+
+
+def task_config(b: Dict[str, Any], template: Optional[Dict[str, Any]] = None) -> Optional[Dict[str, Any]]:
+    """The request's ``config`` (over its template's) restricted to TASK_CONFIG_KEYS; None if empty."""
+    out: Dict[str, Any] = {}
+    for src in (template or {}, b.get("config") or {}):
+        for k in TASK_CONFIG_KEYS:
+            if src.get(k) is not None:
+                out[k] = src[k]
+    return out or None
 
 
 def task_command(kind: str, b: Dict[str, Any]) -> List[str]:
@@ -70,7 +85,7 @@ def add_ntsc_routes(route: Callable[[str, str], Callable], m: Any) -> None:
 
                     raise HTTPError(400, str(e))
                 tid = m.create_command(cmd, int(b.get("slots", 0)), env, kind, b.get("workdir_b64"),
-                                       b.get("resource_pool"), b.get("priority"))
+                                       b.get("resource_pool"), b.get("priority"), task_config=task_config(b))
                 return {"task_id": tid, "type": kind}
             return create
 

@@ -20,7 +20,7 @@ from determined_amd import __version__
 from determined_amd.config import InvalidConfig
 from determined_amd.master._iam import AuthError, _public_user
 from determined_amd.master._iam_routes import add_iam_routes
-from determined_amd.master._ntsc import add_ntsc_routes
+from determined_amd.master._ntsc import add_ntsc_routes, task_config
 from determined_amd.master._exp_routes import add_exp_routes
 from determined_amd.master._runs_routes import add_runs_routes
 from determined_amd.master._webui import add_webui_routes
@@ -483,6 +483,7 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("POST", "/api/v1/commands")
     def create_cmd(q, b):
+        tcfg = None
         if b.get("template"):  # reference api_command.go: the template's config fills what the request lacks
             tcfg = merge_template(m, {}, b["template"])
             res = tcfg.get("resources") or {}
@@ -500,7 +501,8 @@ def build_routes(m: Master) -> List[Route]:
             env.update(b.get("env") or {})
             b["env"] = env or None
         tid = m.create_command(b["command"], int(b.get("slots") or 0), b.get("env"), b.get("type", "COMMAND"),
-                               b.get("workdir_b64"), b.get("resource_pool"), b.get("priority"))
+                               b.get("workdir_b64"), b.get("resource_pool"), b.get("priority"),
+                               task_config=task_config(b, tcfg if b.get("template") else None))
         return {"task_id": tid}
 
     @route("POST", r"/api/v1/tasks/([^/]+)/(pause|unpause)")

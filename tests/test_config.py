@@ -31,7 +31,7 @@ def test_adaptive_asha_defaults():
 
 @pytest.mark.parametrize("bad,msg", [
     ({"searcher": {"name": "random", "metric": "m", "max_length": 5}}, "max_trials"),
-    ({"searcher": {"name": "nope", "metric": "m"}}, "unknown searcher"),
+    ({"searcher": {"name": "nope", "metric": "m"}}, "is one of"),
     ({"searcher": {"name": "single", "max_length": 5}}, "metric"),
     ({"searcher": {"name": "single", "metric": "m", "max_length": {"hours": 3}}}, "max_length"),
     ({"searcher": {"name": "grid", "metric": "m", "max_length": 5},

@@ -36,6 +36,7 @@ def _patch(mp, rank, timeouts_on_rank):
     setattr_(C, "_DB_LOADED", True)
     setattr_(C, "_TUNE_ON", True)
     setattr_(C, "_time_once", lambda fn, reps=3, rounds=2: fn())
+    setattr_(C, "_time_quick", lambda fn: fn())
     setattr_(ops, "ext", lambda: _FakeExt())
     setattr_(ops, "conv_sk_timeouts", lambda device=None: 1 if rank == timeouts_on_rank else 0)
     setattr_(C.torch.cuda, "is_current_stream_capturing", lambda: False)
@@ -91,3 +92,31 @@ def test_other_runtime_errors_propagate(monkeypatch):
 
     with pytest.raises(RuntimeError, match="something else"):
         C._pick(("fwd", "x"), {0: broken, 1: lambda: 1.0}, 0)
+
+
+def _prune_worker(rank, world):
+    """7 candidates: the quick pass (agreed) keeps the near-best ones only, identically on every rank;
+    rank 1's quick time of candidate 4 is noisy-fast but the mean keeps the ranks together."""
+    C = _patch(None, rank, timeouts_on_rank=-1)
+    full_timed = []
+    quick = {0: 9.0, 1: 3.0, 2: 3.3, 3: 8.0, 4: 7.0 if rank == 0 else 1.0, 5: 3.6, 6: 20.0}
+    C._time_quick = lambda fn: fn()[1]
+
+    def full(fn, reps=3, rounds=2):
+        c, _ = fn()
+        full_timed.append(c)
+        return {1: 3.1, 2: 2.9, 5: 3.0, 4: 1.0}[c]
+
+    C._time_once = full
+    cands = {c: (lambda c=c: (c, quick[c])) for c in quick}
+    with C.agree_across_ranks():
+        got = C._pick(("fwd", "p"), cands, 0)
+    return {"got": got, "full": sorted(full_timed)}
+
+
+def test_tuning_prunes_to_agreed_near_best_candidates():
+    outs = run_distributed(_prune_worker, world=2)
+    for o in outs:
+        # agreed quick times: 1 -> 3.0, 2 -> 3.3, 5 -> 3.6, 4 -> 4.0 (> 1.25 x 3.0): 4 is pruned everywhere
+        assert o["full"] == [1, 2, 5]
+        assert o["got"] == 2
