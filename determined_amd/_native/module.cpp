@@ -1,5 +1,6 @@
 // pybind11 bindings for the native control plane (_native.so).
 #include <pybind11/pybind11.h>
+#include <tuple>
 #include <pybind11/stl.h>
 
 #include <sstream>
@@ -214,6 +215,43 @@ PYBIND11_MODULE(_native, m) {
       .value("ROUND_ROBIN", Policy::RoundRobin);
   py::enum_<Fit>(m, "Fit").value("BEST", Fit::Best).value("WORST", Fit::Worst);
 
+  // fair_share.go fairshareSchedule over an explicit snapshot (tests replay the Go vectors with it):
+  // tasks = [(alloc_id, job_id, slots, allocated, preemptible, blocked_agents)] in queue order,
+  // groups = {job_id: (weight, max_slots or -1)}, agents = {agent_id: free slot count}.
+  m.def("fairshare_decide",
+        [](const std::vector<std::tuple<std::string, std::string, int, bool, bool, std::vector<std::string>>>& tasks,
+           const std::map<std::string, std::pair<double, int>>& groups, const std::map<std::string, int>& agents,
+           Fit fit) {
+          std::vector<Request> reqs;
+          int64_t order = 0;
+          for (const auto& t : tasks) {
+            Request r;
+            r.alloc_id = std::get<0>(t);
+            r.job_id = std::get<1>(t);
+            r.slots = std::get<2>(t);
+            r.allocated = std::get<3>(t);
+            r.preemptible = std::get<4>(t);
+            r.excluded_agents = std::get<5>(t);
+            r.order = order++;
+            reqs.push_back(r);
+          }
+          std::map<std::string, FairShareGroup> gs;
+          for (const auto& kv : groups) gs[kv.first] = FairShareGroup{kv.second.first, kv.second.second};
+          std::map<std::string, AgentState> as;
+          for (const auto& kv : agents) {
+            AgentState a;
+            a.id = kv.first;
+            a.num_slots = kv.second;
+            a.slot_owner.assign(kv.second, "");
+            a.slot_disabled.assign(kv.second, 0);
+            a.max_zero_slot_containers = 0;  // the Go mock agents' default
+            as[kv.first] = a;
+          }
+          Decision d = fairshare_decide(reqs, gs, as, fit);
+          return py::make_tuple(d.allocated, d.preempt);
+        },
+        py::arg("tasks"), py::arg("groups"), py::arg("agents"), py::arg("fit") = Fit::Best);
+
   py::class_<Scheduler>(m, "Scheduler")
       .def(py::init<Policy, Fit, bool>(), py::arg("policy"), py::arg("fit") = Fit::Best,
            py::arg("preemption") = true)
@@ -241,6 +279,8 @@ PYBIND11_MODULE(_native, m) {
       .def("remove_request", &Scheduler::remove_request)
       .def("set_priority", &Scheduler::set_priority)
       .def("set_weight", &Scheduler::set_weight)
+      .def("set_max_slots", &Scheduler::set_max_slots)
+      .def("set_agent_max_zero_slot", &Scheduler::set_agent_max_zero_slot)
       .def("schedule",
            [](Scheduler& s) {
              Decision d = s.schedule();

@@ -84,6 +84,18 @@ void Scheduler::set_weight(const std::string& job_id, double weight) {
     if (kv.second.job_id == job_id) kv.second.weight = weight;
 }
 
+void Scheduler::set_max_slots(const std::string& job_id, int max_slots) {
+  if (max_slots < 0)
+    max_slots_.erase(job_id);
+  else
+    max_slots_[job_id] = max_slots;
+}
+
+void Scheduler::set_agent_max_zero_slot(const std::string& id, int n) {
+  auto it = agents_.find(id);
+  if (it != agents_.end()) it->second.max_zero_slot_containers = n;
+}
+
 int Scheduler::total_slots() const {
   int n = 0;
   for (const auto& kv : agents_)
@@ -98,17 +110,19 @@ int Scheduler::used_slots() const {
 }
 
 // fitting_methods.go: BestFit / WorstFit affinity scores (higher is better)
-double Scheduler::score(const Request& r, const AgentState& a) const {
+static double fit_score(const Request& r, const AgentState& a, Fit fit) {
   if (a.used() != 0 || r.slots != 0) {
-    if (fit_ == Fit::Best) return 1.0 / (1.0 + a.empty());
+    if (fit == Fit::Best) return 1.0 / (1.0 + a.empty());
     return a.usable() ? static_cast<double>(a.empty()) / a.usable() : 0.0;
   }
-  return fit_ == Fit::Best ? 1.0 / (1.0 + a.zero_slot_containers) : 1.0 / (1.0 + a.zero_slot_containers);
+  return 1.0 / (1.0 + a.zero_slot_containers);
 }
+
+double Scheduler::score(const Request& r, const AgentState& a) const { return fit_score(r, a, fit_); }
 
 // fitting.go: findFits = shared-agent fit if the request fits one agent, else dedicated
 // whole-agent fits with equal free-slot counts (slots must be a multiple of per-agent slots).
-bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentState>& agents, Fitting* out) const {
+bool find_fit_in(const Request& r, const std::map<std::string, AgentState>& agents, Fit fit, Fitting* out) {
   out->assignment.clear();
   // shared fit
   const AgentState* best = nullptr;
@@ -120,7 +134,8 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
     const AgentState& a = kv.second;
     if (!a.enabled || excluded(a.id)) continue;
     if (r.slots > a.empty()) continue;
-    const double s = score(r, a);
+    if (r.slots == 0 && a.zero_slot_containers >= a.max_zero_slot_containers) continue;
+    const double s = fit_score(r, a, fit);
     if (s > best_score || (s == best_score && best && a.id < best->id)) {
       best = &a;
       best_score = s;
@@ -133,6 +148,7 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
     out->assignment.emplace_back(best->id, slots);
     return true;
   }
+  if (r.slots <= 1) return false;
   // dedicated multi-agent fit: group fully idle agents by slot count
   std::map<int, std::vector<const AgentState*>, std::greater<int>> by_slots;
   for (const auto& kv : agents) {
@@ -155,6 +171,10 @@ bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentStat
     return true;
   }
   return false;
+}
+
+bool Scheduler::find_fit(const Request& r, const std::map<std::string, AgentState>& agents, Fitting* out) const {
+  return find_fit_in(r, agents, fit_, out);
 }
 
 void Scheduler::apply(std::map<std::string, AgentState>& agents, const std::string& alloc_id, const Fitting& f) const {
@@ -264,93 +284,228 @@ Decision Scheduler::schedule_priority() {
   return d;
 }
 
-// fair_share.go: slots are offered to jobs in proportion to their weight (capped at demand,
-// redistributed when a job wants less than its share); tasks of a job start in queue order while
-// the job is under its share; jobs running above their share are preempted (newest task first)
-// when another job is starved.
-Decision Scheduler::schedule_fair_share() {
+// ---------------------------------------------------------------------------------- fair share
+// fair_share.go, step for step: (1) zero-slot tasks start wherever they fit; (2) tasks grouped by job
+// (slot demand capped at the group's max_slots; non-preemptible running slots are "presubscribed");
+// (3) progressive filling (max-min fairness) of slot offers in weight proportion, groups sorted by
+// (demand, registration), with the multi-slot deadlock breaker that disables the newest group that
+// cannot start its smallest task; (4) groups above their offer release preemptible tasks, groups
+// below it start pending tasks that fit.
+namespace {
+
+struct GroupState {
+  std::string job;
+  double weight = 0;
+  int max_slots = -1;
+  bool disabled = false;
+  int demand = 0, active = 0, presubscribed = 0, offered = 0;
+  int64_t registered = 0;  // queue position of the group's first task (JobSubmissionTime)
+  std::vector<const Request*> pending, allocated;
+};
+
+double total_weight(const std::vector<GroupState*>& st) {
+  double t = 0;
+  for (auto* g : st)
+    if (!g->disabled && g->offered < g->demand) t += g->weight;
+  return t;
+}
+
+// Go: int(float64(capacity) * weight / totalWeight) truncates toward zero; a NaN / Inf quotient
+// (all weights 0) converts to the minimum int64 on amd64, so Max(1, .) makes it 1.
+int fair_quota(int capacity, double weight, double total) {
+  const double v = static_cast<double>(capacity) * weight / total;
+  if (!std::isfinite(v)) return 1;
+  return std::max(1, static_cast<int>(v));
+}
+
+void account_preoffers(int& pre, int& offer) {
+  if (pre > 0) {
+    if (pre == offer) {
+      pre = 0;
+      offer = 0;
+    }
+    if (pre > offer) {
+      pre -= offer;
+      offer = 0;
+    }
+    if (pre < offer) {
+      pre = 0;
+      offer -= pre;
+    }
+  }
+}
+
+// The reference sorts its by-time copy with a comparator that indexes the demand-sorted slice
+// (``states[i]``) instead of the copy being sorted; Go's sort.Slice runs insertion sort for fewer
+// than 13 elements, which this reproduces exactly.  Larger lists fall back to the intended order
+// (newest registration first).
+std::vector<GroupState*> go_by_time(const std::vector<GroupState*>& states) {
+  std::vector<GroupState*> out = states;
+  const int n = static_cast<int>(states.size());
+  if (n <= 12) {
+    auto less = [&](int i, int j) { return states[i]->registered > states[j]->registered; };
+    for (int i = 1; i < n; ++i)
+      for (int j = i; j > 0 && less(j, j - 1); --j) std::swap(out[j], out[j - 1]);
+  } else {
+    std::stable_sort(out.begin(), out.end(),
+                     [](const GroupState* a, const GroupState* b) { return a->registered > b->registered; });
+  }
+  return out;
+}
+
+void allocate_offers(std::vector<GroupState*>& states, int capacity) {
+  std::map<GroupState*, int> pre;
+  for (auto* g : states) {
+    if (g->presubscribed == 0) continue;
+    g->offered = g->presubscribed;
+    pre[g] = g->presubscribed;
+    capacity -= g->presubscribed;
+  }
+  std::sort(states.begin(), states.end(), [](const GroupState* a, const GroupState* b) {
+    if (a->demand != b->demand) return a->demand < b->demand;
+    return a->registered < b->registered;
+  });
+  const std::vector<GroupState*> by_time = go_by_time(states);
+  double tw = total_weight(states);
+  for (int left = static_cast<int>(states.size()); left > 0;) {
+    bool progress = false;
+    const int start = capacity;
+    for (auto* g : states) {
+      if (g->disabled || g->offered == g->demand) continue;
+      const int share = fair_quota(start, g->weight, tw);
+      progress = true;
+      int offer = std::min({share, capacity, g->demand - g->offered});
+      account_preoffers(pre[g], offer);
+      g->offered += offer;
+      capacity -= offer;
+      if (g->offered == g->demand) {
+        --left;
+        tw = total_weight(states);
+      }
+    }
+    if (capacity == 0) {
+      bool adjusted = false;
+      for (auto* g : by_time) {
+        const Request* smallest = nullptr;
+        for (const Request* r : g->pending)
+          if (!smallest || r->slots < smallest->slots) smallest = r;
+        if (!g->disabled && g->offered != g->demand && smallest && smallest->slots > g->offered) {
+          capacity += g->offered;
+          g->offered = 0;
+          g->disabled = true;
+          adjusted = true;
+          --left;
+          tw = total_weight(states);
+          break;
+        }
+      }
+      if (!adjusted) return;
+    } else if (!progress) {
+      return;
+    }
+  }
+}
+
+}  // namespace
+
+Decision fairshare_decide(const std::vector<Request>& tasks, const std::map<std::string, FairShareGroup>& groups,
+                          const std::map<std::string, AgentState>& agents, Fit fit) {
   Decision d;
-  struct Group {
-    double weight = 0;
-    int demand = 0, running = 0, share = 0;
-    int64_t first_order = 0;
-    std::vector<Request*> pending, active;
-  };
-  std::map<std::string, Group> groups;
-  for (auto& kv : reqs_) {
-    Request& r = kv.second;
-    Group& g = groups[r.job_id];
-    g.weight = std::max(g.weight, r.weight);
+  Fitting f;
+  for (const Request& r : tasks)
+    if (r.slots == 0 && !r.allocated && find_fit_in(r, agents, fit, &f)) d.allocated.push_back(r.alloc_id);
+  int capacity = 0;
+  for (const auto& kv : agents)
+    if (kv.second.enabled) capacity += kv.second.usable();
+  std::vector<GroupState> store;
+  store.reserve(tasks.size());
+  std::map<std::string, size_t> index;
+  for (const Request& r : tasks) {
+    if (r.slots == 0 || r.slots > capacity) continue;
+    if (!r.allocated && !find_fit_in(r, agents, fit, &f)) continue;
+    auto it = index.find(r.job_id);
+    if (it == index.end()) {
+      GroupState g;
+      g.job = r.job_id;
+      g.registered = r.order;
+      auto gi = groups.find(r.job_id);
+      if (gi != groups.end()) {
+        g.weight = gi->second.weight;
+        g.max_slots = gi->second.max_slots;
+      }
+      it = index.emplace(r.job_id, store.size()).first;
+      store.push_back(g);
+    }
+    GroupState& g = store[it->second];
     g.demand += r.slots;
-    if (g.pending.empty() && g.active.empty()) g.first_order = r.order;
-    g.first_order = std::min(g.first_order, r.order);
-    if (r.allocated) {
-      g.active.push_back(&r);
-      g.running += r.slots;
-    } else {
+    if (!r.allocated) {
       g.pending.push_back(&r);
+    } else {
+      if (!r.preemptible) g.presubscribed += r.slots;
+      g.allocated.push_back(&r);
+      g.active += r.slots;
     }
   }
-  const int capacity = total_slots();
-  // water-filling: give each group min(demand, weight share); redistribute leftovers
-  std::vector<Group*> gs;
-  for (auto& kv : groups) gs.push_back(&kv.second);
-  int remaining = capacity;
-  std::vector<Group*> open = gs;
-  while (remaining > 0 && !open.empty()) {
-    double tw = 0;
-    for (auto* g : open) tw += g->weight;
-    if (tw <= 0) break;
-    std::vector<Group*> next;
-    int handed = 0;
-    for (auto* g : open) {
-      const int want = g->demand - g->share;
-      const int offer = std::max(1, static_cast<int>(std::floor(remaining * g->weight / tw)));
-      const int give = std::min(want, offer);
-      g->share += give;
-      handed += give;
-      if (g->share < g->demand) next.push_back(g);
-    }
-    remaining -= handed;
-    if (handed == 0) break;
-    open = next;
+  std::vector<GroupState*> states;
+  for (auto& g : store) {
+    if (g.max_slots >= 0) g.demand = std::min(g.demand, g.max_slots);
+    states.push_back(&g);
   }
-  std::sort(gs.begin(), gs.end(), [](const Group* a, const Group* b) { return a->first_order < b->first_order; });
-  std::map<std::string, AgentState> local = agents_;
-  bool starved = false;
-  for (auto* g : gs) {
-    std::sort(g->pending.begin(), g->pending.end(), [](const Request* a, const Request* b) { return a->order < b->order; });
-    for (auto* r : g->pending) {
-      if (g->running + r->slots > std::max(g->share, r->slots)) {
-        starved = true;
-        break;
-      }
-      Fitting f;
-      if (!find_fit(*r, local, &f)) {
-        starved = true;
-        break;
-      }
-      apply(local, r->alloc_id, f);
-      r->allocated = true;
-      r->assignment = f.assignment;
-      g->running += r->slots;
-      d.allocated.push_back(r->alloc_id);
-    }
-  }
-  if (preemption_ && starved) {
-    for (auto* g : gs) {
-      if (g->running <= g->share) continue;
-      std::sort(g->active.begin(), g->active.end(), [](const Request* a, const Request* b) { return a->order > b->order; });
-      for (auto* r : g->active) {
-        if (g->running <= g->share) break;
-        if (!r->preemptible || r->preempting) continue;
-        r->preempting = true;
-        g->running -= r->slots;
+  allocate_offers(states, capacity);
+  for (auto* g : states) {
+    if (g->active > g->offered) {
+      for (const Request* r : g->allocated) {
+        if (!r->preemptible) continue;
         d.preempt.push_back(r->alloc_id);
+        g->active -= r->slots;
+        if (g->active <= g->offered) break;
+      }
+    } else if (g->active < g->offered) {
+      g->offered -= g->active;
+      for (const Request* r : g->pending) {
+        if (r->slots > g->offered || !find_fit_in(*r, agents, fit, &f)) continue;
+        d.allocated.push_back(r->alloc_id);
+        g->offered -= r->slots;
       }
     }
   }
-  for (const auto& id : d.allocated) apply(agents_, id, Fitting{reqs_.at(id).assignment});
+  return d;
+}
+
+// The live pool: the fair-share decision on the current queue, then each started task placed on
+// the agents as they are now (one the decision over-committed stays queued for the next pass).
+Decision Scheduler::schedule_fair_share() {
+  std::vector<Request> tasks;
+  for (const auto& kv : reqs_) tasks.push_back(kv.second);
+  std::sort(tasks.begin(), tasks.end(), [](const Request& a, const Request& b) {
+    if (a.order != b.order) return a.order < b.order;
+    return a.alloc_id < b.alloc_id;
+  });
+  std::map<std::string, FairShareGroup> groups;
+  for (const Request& r : tasks) {
+    FairShareGroup& g = groups[r.job_id];
+    g.weight = std::max(g.weight, r.weight);
+    auto ms = max_slots_.find(r.job_id);
+    g.max_slots = ms == max_slots_.end() ? -1 : ms->second;
+  }
+  const Decision raw = fairshare_decide(tasks, groups, agents_, fit_);
+  Decision d;
+  if (preemption_)
+    for (const auto& id : raw.preempt) {
+      Request& r = reqs_.at(id);
+      if (r.preempting) continue;
+      r.preempting = true;
+      d.preempt.push_back(id);
+    }
+  for (const auto& id : raw.allocated) {
+    Request& r = reqs_.at(id);
+    Fitting f;
+    if (r.allocated || !find_fit(r, agents_, &f)) continue;
+    apply(agents_, id, f);
+    r.allocated = true;
+    r.assignment = f.assignment;
+    d.allocated.push_back(id);
+  }
   return d;
 }
 

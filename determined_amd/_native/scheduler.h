@@ -25,6 +25,7 @@ struct AgentState {
   std::vector<std::string> slot_owner;  // allocation id or "" per slot
   std::vector<char> slot_disabled;      // `det slot disable` (reference agentrm slot enable/disable)
   int zero_slot_containers = 0;
+  int max_zero_slot_containers = 1 << 30;  // reference agent max_zero_slot_containers (unlimited here)
   bool enabled = true;
   int empty() const;  // free and enabled slots
   int disabled() const;
@@ -53,6 +54,28 @@ struct Decision {
   std::vector<std::string> preempt;    // alloc ids that must release their resources
 };
 
+struct Fitting {
+  std::vector<std::pair<std::string, std::vector<int>>> assignment;
+};
+
+// fitting.go findFits: a shared fit on one agent (best / worst fit), else whole idle agents of equal
+// free-slot count (multi-slot requests only).
+bool find_fit_in(const Request& r, const std::map<std::string, AgentState>& agents, Fit fit, Fitting* out);
+
+// A job's fair-share parameters (reference tasklist.Group: Weight, MaxSlots).
+struct FairShareGroup {
+  double weight = 0.0;
+  int max_slots = -1;  // < 0: no cap
+};
+
+// fair_share.go fairshareSchedule on a snapshot, decision for decision: ``tasks`` in queue order
+// (``allocated`` = already scheduled), ``groups`` by job id (a job missing from it is a group of
+// weight 0 with no cap, like the Go zero value).  Returns the tasks to start and the preemptible
+// allocations to release.  Like the Go function it checks fits against the unchanged ``agents``
+// (starting several tasks in one call may over-commit; the caller places them one by one).
+Decision fairshare_decide(const std::vector<Request>& tasks, const std::map<std::string, FairShareGroup>& groups,
+                          const std::map<std::string, AgentState>& agents, Fit fit);
+
 class Scheduler {
  public:
   Scheduler(Policy policy, Fit fit, bool preemption) : policy_(policy), fit_(fit), preemption_(preemption) {}
@@ -67,6 +90,8 @@ class Scheduler {
   void remove_request(const std::string& alloc_id);  // frees its slots
   void set_priority(const std::string& job_id, int priority);
   void set_weight(const std::string& job_id, double weight);
+  void set_max_slots(const std::string& job_id, int max_slots);  // fair share group cap (< 0: none)
+  void set_agent_max_zero_slot(const std::string& id, int n);
 
   Decision schedule();
 
@@ -76,9 +101,6 @@ class Scheduler {
   int used_slots() const;
 
  private:
-  struct Fitting {
-    std::vector<std::pair<std::string, std::vector<int>>> assignment;
-  };
   bool find_fit(const Request& r, const std::map<std::string, AgentState>& agents, Fitting* out) const;
   void apply(std::map<std::string, AgentState>& agents, const std::string& alloc_id, const Fitting& f) const;
   void release(std::map<std::string, AgentState>& agents, const Request& r) const;
@@ -93,6 +115,7 @@ class Scheduler {
   bool preemption_;
   std::map<std::string, AgentState> agents_;
   std::map<std::string, Request> reqs_;
+  std::map<std::string, int> max_slots_;
 };
 
 }  // namespace damd_native

@@ -30,6 +30,14 @@
 //   block pair and no atomics.
 //
 // Strides are in elements for (batch, head, token); the head dimension must be contiguous.
+//
+// Key padding (BERT-style batches): an optional byte mask km[b][key] (row stride kms, rows padded to
+// a multiple of 64 keys with zeros) removes keys from every query's softmax; with a mask every key
+// tile takes the masked body.  Dropout on the attention probabilities: keep(b, h, q, k) is a
+// counter-based hash of (seed, b*H + h, q, k) compared with a threshold, recomputed identically by
+// the forward, the dK/dV and the dQ kernels (no mask tensor is stored); kept probabilities are
+// scaled by 1 / (1 - p).  The row sums (l, LSE) use the undropped probabilities, so the backward's
+// delta = rowsum(dO . O) and dS = P . (Z . dP / (1 - p) - delta) hold unchanged.
 
 #include "common.h"
 
@@ -62,11 +70,20 @@ struct Strides {
   int64_t b, h, t;
 };
 
+struct KeyMaskDrop {
+  const uint8_t* km;   // [B][kms] key validity (nullptr: every key < T is valid)
+  int64_t kms;
+  uint32_t seed;       // dropout stream
+  uint32_t thresh;     // drop when hash < thresh (0: no dropout)
+  float inv_keep;      // 1 / (1 - p)
+};
+
 struct FwdArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
   Strides sq, sk, sv, so;
   int H, T;
   float scale_log2;  // softmax scale * log2(e)
+  KeyMaskDrop md;
 };
 
 struct BwdArgs {
@@ -75,7 +92,19 @@ struct BwdArgs {
   Strides sq, sk, sv, sdo, sdk, sdv;
   int H, T;
   float scale, scale_log2;
+  KeyMaskDrop md;
 };
+
+// dropout decision for (b*H + h, query, key): murmur3-style finalizer of the mixed counters
+__device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t thresh, uint32_t bh, uint32_t q, uint32_t k) {
+  uint32_t x = seed ^ (bh * 0x9E3779B1u) ^ (q * 0x85EBCA77u) ^ (k * 0xC2B2AE3Du);
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x >= thresh;
+}
 
 __device__ __forceinline__ f4 mfma(s8 a, s8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
@@ -151,7 +180,7 @@ struct Stage {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
   constexpr int KP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
@@ -164,6 +193,8 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
   const bf16_t* Qp = a.q + b * a.sq.b + h * a.sq.h;
   const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
   const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
+  const uint8_t* KMp = a.md.km ? a.md.km + b * a.md.kms : nullptr;
+  const uint32_t bh32 = static_cast<uint32_t>(b * a.H + h);
 
   s8 qf[kQT][D / 32];
 #pragma unroll
@@ -193,7 +224,7 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
   // Leading tiles that no row of the workgroup masks (all keys < T and <= q0) run a body
   // compiled without any masking code; only the <= 2 diagonal / ragged tiles carry the selects.
   // (D = 128: a single masked body -- the unmasked copy pushes it to 256 VGPRs, 1 wave / SIMD)
-  const int kb_full = D == 64 ? min(kb_end, CAUSAL ? min((q0 + 1) / kBlk, T / kBlk) : T / kBlk) : 0;
+  const int kb_full = D == 64 && !KMp ? min(kb_end, CAUSAL ? min((q0 + 1) / kBlk, T / kBlk) : T / kBlk) : 0;
   auto tile = [&](int kb, auto masked) {
     constexpr bool MASK = decltype(masked)::value;
     const int k0 = kb * kBlk;
@@ -230,6 +261,14 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             s[qt][nt][r] = (k0 + nt * 16 + 4 * g + r > kmax) ? -INFINITY : s[qt][nt][r];
+        if (KMp) {  // padded keys (row padded to a multiple of 64: the word loads stay in bounds)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const uint32_t mw = *reinterpret_cast<const uint32_t*>(KMp + k0 + nt * 16 + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[qt][nt][r] = ((mw >> (8 * r)) & 0xffu) ? s[qt][nt][r] : -INFINITY;
+          }
+        }
       }
       float mx = -INFINITY;
 #pragma unroll
@@ -247,8 +286,11 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -m_use));
-          s[qt][nt][r] = p;
           rs += p;
+          if constexpr (DROP)
+            s[qt][nt][r] = drop_keep(a.md.seed, a.md.thresh, bh32, myq, k0 + nt * 16 + 4 * g + r) ? p : 0.f;
+          else
+            s[qt][nt][r] = p;
         }
       }
       l[qt] = l[qt] * alpha + rs;
@@ -279,7 +321,7 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
     lt += __shfl_xor(lt, 32, 64);
     const int myq = qw + qt * 16 + c;
     if (myq < T) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      const float inv = lt > 0.f ? (DROP ? a.md.inv_keep : 1.f) / lt : 0.f;
       bf16_t* Op = a.o + b * a.so.b + h * a.so.h + static_cast<int64_t>(myq) * a.so.t;
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
@@ -320,7 +362,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
   if (row < rows && part == 0) delta[row] = acc;
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
   constexpr int RP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[kBlk * RP];
@@ -337,6 +379,8 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
   const bf16_t* dOp = a.dout + b * a.sdo.b + h * a.sdo.h;
   const int64_t bh = static_cast<int64_t>(b) * a.H + h;
   const int mykey = k0 + w * 16 + c;
+  const uint8_t* KMp = a.md.km ? a.md.km + b * a.md.kms : nullptr;
+  const bool kvalid = mykey < T && (KMp == nullptr || KMp[mykey] != 0);
 
   s8 kf[D / 32], vf[D / 32];
 #pragma unroll
@@ -373,7 +417,7 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
       ost.load(dOp, a.sdo.t, q0 + kBlk, T);
     }
 
-    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && q0 < k0 + kBlk);
+    const bool need_mask = (k0 + kBlk > T) || (CAUSAL && q0 < k0 + kBlk) || KMp != nullptr;
     f4 P[4], dS[4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -389,9 +433,15 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int ql = qt * 16 + 4 * g + r;
         float p = ex2(fmaf(sacc[r], a.scale_log2, -lse2[ql]));
-        if (need_mask) p = (mykey >= T || (CAUSAL && mykey > q0 + ql)) ? 0.f : p;
-        P[qt][r] = p;
-        dS[qt][r] = p * (dpacc[r] - dl[ql]);
+        if (need_mask) p = (!kvalid || (CAUSAL && mykey > q0 + ql)) ? 0.f : p;
+        if constexpr (DROP) {
+          const bool keep = drop_keep(a.md.seed, a.md.thresh, static_cast<uint32_t>(bh), q0 + ql, mykey);
+          P[qt][r] = keep ? p * a.md.inv_keep : 0.f;  // dV uses the dropped, rescaled probabilities
+          dS[qt][r] = p * ((keep ? dpacc[r] * a.md.inv_keep : 0.f) - dl[ql]);
+        } else {
+          P[qt][r] = p;
+          dS[qt][r] = p * (dpacc[r] - dl[ql]);
+        }
       }
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = 32 queries per step, permuted order)
@@ -429,10 +479,11 @@ struct DqArgs {
   Strides sq, sk, sv, sdo, sdq;
   int H, T;
   float scale, scale_log2;
+  KeyMaskDrop md;
 };
 
 // dQ for a block of kFwdRows query rows (same wave / lane layout as the forward).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
   constexpr int KP = kLdsStride(D);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[kBlk * KP];
@@ -447,6 +498,7 @@ __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
   const bf16_t* Kp = a.k + b * a.sk.b + h * a.sk.h;
   const bf16_t* Vp = a.v + b * a.sv.b + h * a.sv.h;
   const bf16_t* dOp = a.dout + b * a.sdo.b + h * a.sdo.h;
+  const uint8_t* KMp = a.md.km ? a.md.km + b * a.md.kms : nullptr;
 
   s8 qf[kQT][D / 32], of[kQT][D / 32];
   float lse2[kQT], dl[kQT];
@@ -512,11 +564,17 @@ __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
       const int kmax = CAUSAL ? min(T - 1, myq) : T - 1;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
+        const uint32_t mw = KMp ? *reinterpret_cast<const uint32_t*>(KMp + k0 + nt * 16 + 4 * g) : 0xffffffffu;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          const int key = k0 + nt * 16 + 4 * g + r;
           float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -lse2[qt]));
-          if (need_mask) p = (k0 + nt * 16 + 4 * g + r > kmax) ? 0.f : p;
-          s[qt][nt][r] = p * (dp[qt][nt][r] - dl[qt]);  // dS^T
+          if (need_mask) p = (key > kmax) ? 0.f : p;
+          p = ((mw >> (8 * r)) & 0xffu) ? p : 0.f;
+          float dpv = dp[qt][nt][r];
+          if constexpr (DROP)
+            dpv = drop_keep(a.md.seed, a.md.thresh, static_cast<uint32_t>(bh), myq, key) ? dpv * a.md.inv_keep : 0.f;
+          s[qt][nt][r] = p * (dpv - dl[qt]);  // dS^T
         }
       }
     }
@@ -558,30 +616,59 @@ using namespace damd::attn;
 
 extern "C" {
 
-// strides: 4 tensors (q, k, v, o) x (b, h, t) in elements
+#define DAMD_ATTN_DISPATCH(KERNEL, GRID, ARGS)                                                       \
+  do {                                                                                               \
+    const bool drop_ = (ARGS).md.thresh != 0;                                                        \
+    if (D == 64) {                                                                                   \
+      if (causal) {                                                                                  \
+        if (drop_) DAMD_LAUNCH((KERNEL<64, true, true>), GRID, dim3(kThreads), 0, st, ARGS);         \
+        else DAMD_LAUNCH((KERNEL<64, true, false>), GRID, dim3(kThreads), 0, st, ARGS);              \
+      } else {                                                                                       \
+        if (drop_) DAMD_LAUNCH((KERNEL<64, false, true>), GRID, dim3(kThreads), 0, st, ARGS);        \
+        else DAMD_LAUNCH((KERNEL<64, false, false>), GRID, dim3(kThreads), 0, st, ARGS);             \
+      }                                                                                              \
+    } else {                                                                                         \
+      if (causal) {                                                                                  \
+        if (drop_) DAMD_LAUNCH((KERNEL<128, true, true>), GRID, dim3(kThreads), 0, st, ARGS);        \
+        else DAMD_LAUNCH((KERNEL<128, true, false>), GRID, dim3(kThreads), 0, st, ARGS);             \
+      } else {                                                                                       \
+        if (drop_) DAMD_LAUNCH((KERNEL<128, false, true>), GRID, dim3(kThreads), 0, st, ARGS);       \
+        else DAMD_LAUNCH((KERNEL<128, false, false>), GRID, dim3(kThreads), 0, st, ARGS);            \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
+
+static KeyMaskDrop make_md(const uint8_t* km, int64_t kms, uint32_t seed, float drop_p) {
+  KeyMaskDrop md;
+  md.km = km;
+  md.kms = kms;
+  md.seed = seed;
+  const double t = static_cast<double>(drop_p) * 4294967296.0;
+  md.thresh = drop_p > 0.f ? static_cast<uint32_t>(t >= 4294967295.0 ? 4294967295.0 : (t < 1.0 ? 1.0 : t)) : 0u;
+  md.inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  return md;
+}
+
+// strides: 4 tensors (q, k, v, o) x (b, h, t) in elements; km: optional [B][kms] key mask
 void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
-                          int B, int H, int T, int D, float scale, int causal, hipStream_t st) {
+                          int B, int H, int T, int D, float scale, int causal, const uint8_t* km, int64_t kms,
+                          uint32_t seed, float drop_p, hipStream_t st) {
   FwdArgs a;
   a.q = static_cast<const bf16_t*>(q); a.k = static_cast<const bf16_t*>(k); a.v = static_cast<const bf16_t*>(v);
   a.o = static_cast<bf16_t*>(o); a.lse = lse;
   a.sq = {strides[0], strides[1], strides[2]}; a.sk = {strides[3], strides[4], strides[5]};
   a.sv = {strides[6], strides[7], strides[8]}; a.so = {strides[9], strides[10], strides[11]};
   a.H = H; a.T = T; a.scale_log2 = scale * kLog2e;
+  a.md = make_md(km, kms, seed, drop_p);
   dim3 grid((T + kFwdRows - 1) / kFwdRows, H, B);
-  if (D == 64) {
-    if (causal) DAMD_LAUNCH((attn_fwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
-    else DAMD_LAUNCH((attn_fwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
-  } else {
-    if (causal) DAMD_LAUNCH((attn_fwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
-    else DAMD_LAUNCH((attn_fwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
-  }
-  DAMD_CHECK_LAUNCH();
+  DAMD_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
 }
 
 // strides: 8 tensors (q, k, v, o, dout, dk, dv, dq) x (b, h, t)
 void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                           const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
-                          const int64_t* s, int B, int H, int T, int D, float scale, int causal, hipStream_t st) {
+                          const int64_t* s, int B, int H, int T, int D, float scale, int causal,
+                          const uint8_t* km, int64_t kms, uint32_t seed, float drop_p, hipStream_t st) {
   const Strides sq{s[0], s[1], s[2]}, sk{s[3], s[4], s[5]}, sv{s[6], s[7], s[8]}, so{s[9], s[10], s[11]},
       sdo{s[12], s[13], s[14]}, sdk{s[15], s[16], s[17]}, sdv{s[18], s[19], s[20]}, sdq{s[21], s[22], s[23]};
   const int64_t rows = static_cast<int64_t>(B) * H * T;
@@ -603,29 +690,17 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   a.dk = static_cast<bf16_t*>(dk); a.dv = static_cast<bf16_t*>(dv);
   a.sq = sq; a.sk = sk; a.sv = sv; a.sdo = sdo; a.sdk = sdk; a.sdv = sdv;
   a.H = H; a.T = T; a.scale = scale; a.scale_log2 = scale * kLog2e;
+  a.md = make_md(km, kms, seed, drop_p);
   dim3 grid((T + kBlk - 1) / kBlk, H, B);
-  if (D == 64) {
-    if (causal) DAMD_LAUNCH((attn_bwd_kernel<64, true>), grid, dim3(kThreads), 0, st, a);
-    else DAMD_LAUNCH((attn_bwd_kernel<64, false>), grid, dim3(kThreads), 0, st, a);
-  } else {
-    if (causal) DAMD_LAUNCH((attn_bwd_kernel<128, true>), grid, dim3(kThreads), 0, st, a);
-    else DAMD_LAUNCH((attn_bwd_kernel<128, false>), grid, dim3(kThreads), 0, st, a);
-  }
-  DAMD_CHECK_LAUNCH();
+  DAMD_ATTN_DISPATCH(attn_bwd_kernel, grid, a);
   DqArgs d;
   d.q = a.q; d.k = a.k; d.v = a.v; d.dout = a.dout; d.lse = lse; d.delta = delta;
   d.dq = static_cast<bf16_t*>(dq);
   d.sq = sq; d.sk = sk; d.sv = sv; d.sdo = sdo; d.sdq = sdq;
   d.H = H; d.T = T; d.scale = scale; d.scale_log2 = scale * kLog2e;
+  d.md = a.md;
   dim3 qgrid((T + kFwdRows - 1) / kFwdRows, H, B);
-  if (D == 64) {
-    if (causal) DAMD_LAUNCH((attn_dq_kernel<64, true>), qgrid, dim3(kThreads), 0, st, d);
-    else DAMD_LAUNCH((attn_dq_kernel<64, false>), qgrid, dim3(kThreads), 0, st, d);
-  } else {
-    if (causal) DAMD_LAUNCH((attn_dq_kernel<128, true>), qgrid, dim3(kThreads), 0, st, d);
-    else DAMD_LAUNCH((attn_dq_kernel<128, false>), qgrid, dim3(kThreads), 0, st, d);
-  }
-  DAMD_CHECK_LAUNCH();
+  DAMD_ATTN_DISPATCH(attn_dq_kernel, qgrid, d);
 }
 
 }  // extern "C"

@@ -171,10 +171,10 @@ extern "C" int damd_stem_wgrad_blocks(int64_t, int);
 extern "C" void damd_stem_wgrad_launch(const void*, const void*, float*, void*, int, int64_t, int, int, hipStream_t);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
-                                     int, int, float, int, hipStream_t);
+                                     int, int, float, int, const uint8_t*, int64_t, uint32_t, float, hipStream_t);
 extern "C" void damd_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*,
                                      float*, float*, void*, void*, void*, const int64_t*, int, int, int, int, float,
-                                     int, hipStream_t);
+                                     int, const uint8_t*, int64_t, uint32_t, float, hipStream_t);
 // launchers (fused.hip)
 extern "C" void damd_lm_ce_fwd_launch(const void*, const int64_t*, int64_t, int, int, int, int64_t, float*, float*,
                                       hipStream_t);
@@ -1351,11 +1351,29 @@ void push_strides(std::vector<int64_t>& s, const at::Tensor& t) {
   s.push_back(t.stride(2));
 }
 
+// Optional key-padding mask: uint8 [B, Tpad] (contiguous rows, Tpad a multiple of 64 and >= T;
+// zero = padded key).  Dropout: probability drop_p in [0, 1) with a 32-bit seed.
+const uint8_t* check_kmask(const c10::optional<at::Tensor>& km, const at::Tensor& q, int64_t* stride) {
+  *stride = 0;
+  if (!km.has_value() || !km->defined()) return nullptr;
+  const at::Tensor& m = *km;
+  TORCH_CHECK(m.is_cuda() && m.scalar_type() == at::kByte && m.dim() == 2 && m.stride(1) == 1,
+              "key mask: uint8 [B, Tpad] with contiguous rows");
+  TORCH_CHECK(m.size(0) == q.size(0) && m.size(1) >= q.size(2) && m.size(1) % 64 == 0 && m.stride(0) % 64 == 0,
+              "key mask: [B, Tpad] with Tpad >= T a multiple of 64");
+  TORCH_CHECK(m.device() == q.device(), "key mask on another device");
+  *stride = m.stride(0);
+  return m.data_ptr<uint8_t>();
+}
+
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
-                                 double scale) {
+                                 double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed) {
   check_attn(q, q, "q");
   check_attn(k, q, "k");
   check_attn(v, q, "v");
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "dropout probability must be in [0, 1)");
+  int64_t kms = 0;
+  const uint8_t* km = check_kmask(kmask, q, &kms);
   const int64_t B = q.size(0), H = q.size(1), T = q.size(2), D = q.size(3);
   // output in [B, T, H, D] memory (so "merge heads" is a free view), returned as [B, H, T, D]
   auto o = at::empty({B, T, H, D}, q.options()).permute({0, 2, 1, 3});
@@ -1368,13 +1386,14 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   if (B * H * T > 0)
     damd_attn_fwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), s.data(),
                          static_cast<int>(B), static_cast<int>(H), static_cast<int>(T), static_cast<int>(D),
-                         static_cast<float>(scale), causal ? 1 : 0, cur_stream());
+                         static_cast<float>(scale), causal ? 1 : 0, km, kms, static_cast<uint32_t>(seed),
+                         static_cast<float>(drop_p), cur_stream());
   return {o, lse};
 }
 
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               const at::Tensor& o, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, bool causal,
-              double scale) {
+              double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed) {
   check_attn(q, q, "q");
   check_attn(k, q, "k");
   check_attn(v, q, "v");
@@ -1386,6 +1405,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   const int64_t B = q.size(0), H = q.size(1), T = q.size(2), D = q.size(3);
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse [B,H,T] f32");
   auto delta = at::empty({B, H, T}, lse.options());
+  int64_t kms = 0;
+  const uint8_t* km = check_kmask(kmask, q, &kms);
 
   std::vector<int64_t> s;
   const at::Tensor* order[] = {&q, &k, &v, &o, &dout, &dk, &dv, &dq};
@@ -1395,7 +1416,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
                          lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr, dq.data_ptr(),
                          dk.data_ptr(), dv.data_ptr(), s.data(), static_cast<int>(B), static_cast<int>(H),
                          static_cast<int>(T), static_cast<int>(D), static_cast<float>(scale), causal ? 1 : 0,
-                         cur_stream());
+                         km, kms, static_cast<uint32_t>(seed), static_cast<float>(drop_p), cur_stream());
 }
 
 // ---------------------------------------------------------------- fused LM loss / bias grad
@@ -1499,8 +1520,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("debug_launch", &debug_launch, "launch-check probe: mode 0 valid, 1 LDS over the limit, 2 oversized block");
   m.def("gelu_bwd_bias", &gelu_bwd_bias);
   m.def("attn_supported", &attn_supported);
-  m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("scale"),
+        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"), py::arg("scale"),
+        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
   m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);

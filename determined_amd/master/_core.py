@@ -588,6 +588,7 @@ class Master:
         tr.allocation = a
         self.allocations[aid] = a
         prio = exp.config["resources"].get("priority")
+        self.sched.set_max_slots(f"exp-{exp.id}", exp.config["resources"].get("max_slots"))
         self.sched.add_request(aid, f"exp-{exp.id}", slots, int(prio) if prio is not None else 42,
                                float(exp.config["resources"].get("weight", 1)), self._next_order(), True,
                                list(tr.excluded_agents), pool=exp.config["resources"].get("resource_pool") or None)
@@ -704,6 +705,7 @@ class Master:
             res = exp.config.setdefault("resources", {})
             if max_slots != "unset":
                 res["max_slots"] = None if max_slots is None else int(max_slots)
+                self.sched.set_max_slots(f"exp-{eid}", res["max_slots"])
             if weight is not None:
                 res["weight"] = float(weight)
                 self.sched.set_weight(f"exp-{eid}", float(weight))

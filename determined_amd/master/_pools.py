@@ -130,6 +130,11 @@ class PoolSet:
         for p in self.pools.values():
             p.sched.set_weight(job_id, weight)
 
+    def set_max_slots(self, job_id: str, max_slots: Optional[int]) -> None:
+        """Fair-share group cap of a job (experiment ``resources.max_slots``; None: uncapped)."""
+        for p in self.pools.values():
+            p.sched.set_max_slots(job_id, -1 if max_slots is None else int(max_slots))
+
     def schedule(self) -> Dict[str, List[str]]:
         out: Dict[str, List[str]] = {"allocated": [], "preempt": []}
         for p in self.pools.values():

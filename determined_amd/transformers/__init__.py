@@ -6,3 +6,4 @@ from determined_amd.transformers._hf_callback import (
     get_metric_type,
 )
 from determined_amd.transformers._optim import fused_optimizer
+from determined_amd.transformers._kernels import accelerate

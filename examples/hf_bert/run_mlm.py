@@ -6,7 +6,9 @@ Model: ``BertForMaskedLM`` from ``BertConfig()`` (bert-base-uncased shape, 110M 
 random init -- no checkpoint downloads are possible).  Data: synthetic token sequences with
 BERT-style 15% masking (80% [MASK] / 10% random / 10% kept).  Optimizer: the fused
 single-launch AdamW (``determined_amd.transformers.fused_optimizer``) unless
-``--hf_optimizer`` is given.
+``--hf_optimizer`` is given.  Kernels: ``determined_amd.transformers.accelerate`` routes attention
+(key-padding mask + in-kernel dropout) through csrc/attention.hip and residual + dropout + LayerNorm
+through csrc/norm.hip unless ``--stock_kernels`` is given.
 
 On-cluster:   python -m determined_amd.launch.torch_distributed python run_mlm.py [HF args]
 Off-cluster:  python run_mlm.py --output_dir /tmp/bert --max_steps 50 ...
@@ -25,7 +27,7 @@ from torch.utils.data import Dataset
 
 from determined_amd import core
 from determined_amd._info import get_cluster_info
-from determined_amd.transformers import DetCallback, fused_optimizer
+from determined_amd.transformers import DetCallback, accelerate, fused_optimizer
 
 logger = logging.getLogger("run_mlm")
 
@@ -66,6 +68,9 @@ class ModelArguments:
     train_samples: int = 1_000_000
     eval_samples: int = 2048
     hf_optimizer: bool = False
+    stock_kernels: bool = False
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.1
 
 
 def dict2args(d: Dict[str, Any]) -> List[str]:
@@ -85,8 +90,12 @@ def build_model(m: ModelArguments, bf16: bool) -> torch.nn.Module:
     cfg = transformers.BertConfig(hidden_size=m.hidden_size, num_hidden_layers=m.num_hidden_layers,
                                   num_attention_heads=m.num_attention_heads, intermediate_size=m.intermediate_size,
                                   vocab_size=m.vocab_size, max_position_embeddings=max(512, m.seq_len),
+                                  hidden_dropout_prob=m.hidden_dropout_prob,
+                                  attention_probs_dropout_prob=m.attention_probs_dropout_prob,
                                   attn_implementation="sdpa")
     model = transformers.BertForMaskedLM(cfg)
+    if not m.stock_kernels:
+        accelerate(model)
     return model
 
 

@@ -12,7 +12,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TESTS = ["tests/test_native_loader.py", "tests/test_scheduler.py", "tests/test_searcher.py",
-         "tests/test_searcher_go_vectors.py"]
+         "tests/test_searcher_go_vectors.py", "tests/test_scheduler_go_vectors.py"]
 
 
 @pytest.mark.slow

@@ -74,6 +74,10 @@ def test_priority_without_preemption_waits():
 
 
 def test_fair_share_splits_between_jobs():
+    """Reference fair_share.go semantics: tasks that fit nowhere right now are left out of the share
+    computation (calculateGroupStates), so a full node is not rebalanced until a slot frees; then
+    the starved job enters the share, the job above its share releases tasks (oldest first, like
+    the reference's allocatedReqs order) and the starved job takes the freed slots."""
     s = sched("fair_share")
     s.add_agent("n", 8)
     for i in range(8):
@@ -81,12 +85,14 @@ def test_fair_share_splits_between_jobs():
     assert len(s.schedule()["allocated"]) == 8
     for i in range(8):
         s.add_request(f"b{i}", "B", 1, order=100 + i)
+    assert s.schedule() == {"allocated": [], "preempt": []}
+    s.remove_request("a7")  # one A task finishes: B now fits and enters the share
     d = s.schedule()
-    assert len(d["preempt"]) == 4  # A gives back half of the node to B
+    assert d["allocated"] == ["b0"] and d["preempt"] == ["a0", "a1", "a2"]
     for aid in d["preempt"]:
         s.remove_request(aid)
     d = s.schedule()
-    assert len(d["allocated"]) == 4 and all(a.startswith("b") for a in d["allocated"])
+    assert d["allocated"] == ["b1", "b2", "b3"] and d["preempt"] == []
 
 
 def test_round_robin_fifo_blocks():
