@@ -1,6 +1,7 @@
 """``det notebook|shell|tensorboard|command`` and ``det master config|logs`` (reference:
 ``harness/determined/cli/{notebook,shell,tensorboard,command,master}.py``)."""
 
+import argparse
 import json
 import os
 import shlex
@@ -126,7 +127,13 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
             sh_open(a)
 
     def sh_open(a):
-        t = _wait_proxy(session(a), a.task_id)
+        s = session(a)
+        t = _wait_proxy(s, a.task_id)
+        if (t.get("proxy") or {}).get("tunnel"):  # the task's PTY server, through the master
+            from determined_amd.cli import _tunnel
+
+            cmd = [c for c in (getattr(a, "command", None) or []) if c != "--"]
+            sys.exit(_tunnel.run(s.master_url, a.task_id, cmd or None, token=s.token))
         sc = shell_command(t)
         env = dict(os.environ)
         env.update(sc["env"])
@@ -134,7 +141,11 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
         sys.exit(rc)
 
     def sh_ssh(a):
-        sc = shell_command(_wait_proxy(session(a), a.task_id))
+        t = _wait_proxy(session(a), a.task_id)
+        if (t.get("proxy") or {}).get("tunnel"):
+            print(f"det -m {a.master} shell open {a.task_id}   # tunnelled through the master, no ssh needed")
+            return
+        sc = shell_command(t)
         print(shlex.join(sc["argv"]) if sc["argv"][0] == "ssh" else
               " ".join(f"{k}={shlex.quote(v)}" for k, v in sc["env"].items()) + " bash -i")
 
@@ -144,6 +155,8 @@ def register(sub: Any, session: Any, show: Any, follow_logs: Any) -> None:
     for verb, fn in (("open", sh_open), ("show-ssh-command", sh_ssh)):
         o = g.add_parser(verb)
         o.add_argument("task_id")
+        if verb == "open":
+            o.add_argument("command", nargs=argparse.REMAINDER, help="run this instead of a login shell")
         o.set_defaults(fn=fn)
 
     # ---------------------------------------------------------------- master config / logs

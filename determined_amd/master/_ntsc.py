@@ -94,7 +94,9 @@ def add_ntsc_routes(route: Callable[[str, str], Callable], m: Any) -> None:
     for plural, kind in KINDS.items():
         def make_list(kind=kind):
             def lst(q, b):
-                rows = m.db.all("SELECT * FROM tasks WHERE type=? ORDER BY start_time", [kind])
+                from determined_amd.master._server import public_task
+
+                rows = [public_task(r) for r in m.db.all("SELECT * FROM tasks WHERE type=? ORDER BY start_time", [kind])]
                 return {"tasks": rows}
             return lst
 

@@ -537,7 +537,10 @@ def build_routes(m: Master) -> List[Route]:
         port = b.get("port")
         if port is not None and not (isinstance(port, int) and 0 < port < 65536):
             raise HTTPError(400, f"invalid proxy port {port!r}")
-        m.db.update("tasks", "id", task_id, proxy={"host": host, "port": port, "cwd": b.get("cwd"), "env": b.get("env")})
+        px = {"host": host, "port": port, "cwd": b.get("cwd"), "env": b.get("env")}
+        if b.get("tunnel"):  # a shell server (exec/shell.py): reached only through /proxy/<task>/_tunnel
+            px.update(tunnel=True, shell_key=str(b.get("shell_key") or ""))
+        m.db.update("tasks", "id", task_id, proxy=px)
         return {}
 
     add_ntsc_routes(route, m)
@@ -546,14 +549,14 @@ def build_routes(m: Master) -> List[Route]:
 
     @route("GET", "/api/v1/tasks")
     def list_tasks(q, b):
-        return {"tasks": m.db.all("SELECT * FROM tasks ORDER BY start_time")}
+        return {"tasks": [public_task(r) for r in m.db.all("SELECT * FROM tasks ORDER BY start_time")]}
 
     @route("GET", r"/api/v1/tasks/([^/]+)")
     def get_task(q, b, task_id):
         row = m.db.one("SELECT * FROM tasks WHERE id=?", [task_id])
         if row is None:
             raise HTTPError(404, f"task {task_id} not found")
-        return {"task": row}
+        return {"task": public_task(row)}
 
     @route("POST", r"/api/v1/tasks/([^/]+)/kill")
     def kill_task(q, b, task_id):
@@ -833,6 +836,14 @@ def build_routes(m: Master) -> List[Route]:
 _LOOPBACK = frozenset(("127.0.0.1", "localhost", "::1"))
 
 
+def public_task(row: Dict[str, Any]) -> Dict[str, Any]:
+    """A task row as the API shows it: a shell server's key stays inside the master."""
+    px = row.get("proxy")
+    if isinstance(px, dict) and "shell_key" in px:
+        row = dict(row, proxy={k: v for k, v in px.items() if k != "shell_key"})
+    return row
+
+
 def _may_use_proxy(iam: Any, task_cfg: Dict[str, Any]) -> bool:
     """Reference ``processProxyAuthentication`` (CanGetNSC / CanGetTensorboard): the owner and admins
     always; in rbac mode also users with view permission on the task's workspace."""
@@ -890,6 +901,11 @@ class _Handler(BaseHTTPRequestHandler):
             px = row.get("proxy")
             if not px or not px.get("port"):
                 raise HTTPError(404, f"task {task_id} has no proxied service (yet)")
+            if rest == "/_tunnel":
+                self._tunnel(px)
+                return
+            if px.get("tunnel"):
+                raise HTTPError(400, f"task {task_id} serves a shell: connect with `det shell open {task_id}`")
             conn = http.client.HTTPConnection(px.get("host") or "127.0.0.1", int(px["port"]), timeout=60)
             hdrs = {k: v for k, v in self.headers.items() if k.lower() not in ("host", "authorization", "content-length",
                                                                              "connection", "cookie")}
@@ -921,6 +937,42 @@ class _Handler(BaseHTTPRequestHandler):
             self.send_header("Content-Length", str(len(data)))
             self.end_headers()
             self.wfile.write(data)
+
+    def _tunnel(self, px: Dict[str, Any]) -> None:
+        """``/proxy/<task>/_tunnel`` with ``Upgrade: damd-tunnel``: a raw byte stream to the task's
+        shell server (exec/shell.py).  The user is already authorised for the task (``_proxy``); the
+        master sends the task's shell key as the first line, answers 101 and relays both ways until
+        either side closes (reference: the master's TCP proxy behind ``det shell``'s ssh tunnel)."""
+        import select
+        import socket
+
+        if (self.headers.get("Upgrade") or "").lower() != "damd-tunnel" or not px.get("tunnel"):
+            raise HTTPError(400, "this endpoint needs 'Upgrade: damd-tunnel' on a shell task")
+        up = socket.create_connection((px.get("host") or "127.0.0.1", int(px["port"])), timeout=10)
+        up.settimeout(None)
+        up.sendall(b"DAMD-SHELL " + str(px.get("shell_key") or "").encode() + b"\n")
+        self.send_response(101)
+        self.send_header("Upgrade", "damd-tunnel")
+        self.send_header("Connection", "Upgrade")
+        self.end_headers()
+        self.wfile.flush()
+        self.close_connection = True
+        down = self.connection
+        try:
+            while True:
+                r, _, _ = select.select([down, up], [], [], 60)
+                if not r:
+                    continue
+                for src, dst in ((down, up), (up, down)):
+                    if src in r:
+                        data = src.recv(65536)
+                        if not data:
+                            return
+                        dst.sendall(data)
+        except OSError:
+            return
+        finally:
+            up.close()
 
     def _dispatch(self, method: str) -> None:
         parsed = urllib.parse.urlparse(self.path)
