@@ -24,7 +24,13 @@ def test_webui_page_is_served(master):
         with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}{path}", timeout=10) as r:
             assert r.headers["Content-Type"].startswith("text/html")
             body = r.read().decode()
-        assert "determined-amd" in body and "/api/v1/stream" in body and "/api/v1/experiments" in body
+        assert "determined-amd" in body and "/ui/app.js" in body and "#/runs" in body and "#/jobs" in body
+    with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/ui/app.js", timeout=10) as r:
+        assert r.headers["Content-Type"].startswith("application/javascript")
+        js = r.read().decode()
+    assert "/api/v1/stream" in js and "/api/v1/runs" in js and "parallel(" in js
+    with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/ui/app.css", timeout=10) as r:
+        assert r.headers["Content-Type"].startswith("text/css")
 
 
 def test_stream_long_poll_delivers_entity_changes(master):
@@ -65,25 +71,33 @@ def test_stream_long_poll_delivers_entity_changes(master):
 
 @pytest.mark.skipif(__import__("shutil").which("node") is None, reason="node not installed")
 def test_webui_script_renders_every_view_against_a_live_master(master, tmp_path):
-    """Run the page's script under node with a minimal DOM stub: every view renders from the real
-    API responses without a script error."""
+    """Run the app's script under node with a minimal DOM stub: every view (and every experiment
+    tab) renders from the real API responses without a script error."""
     import json
     import subprocess
 
-    from determined_amd.master._webui import PAGE
+    from determined_amd.master._webui import ASSETS
 
     srv, s = master
-    cfg = {"name": "ui", "entrypoint": "model_def:T", "hyperparameters": {"lr": 0.1},
-           "searcher": {"name": "single", "metric": "loss", "max_length": {"batches": 1}}}
-    eid = s.post("/api/v1/experiments", {"config": cfg, "activate": False})["experiment"]["id"]
-    js = PAGE.split("<script>")[1].split("</script>")[0]
+    cfg = {"name": "ui", "entrypoint": "model_def:T", "hyperparameters": {"lr": {"type": "double", "minval": 0.001,
+                                                                                  "maxval": 0.1}, "opt": "sgd"},
+           "searcher": {"name": "random", "metric": "loss", "max_trials": 3, "max_length": {"batches": 1}}}
+    eid = s.post("/api/v1/experiments", {"config": cfg})["experiment"]["id"]
+    trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+    assert trials
+    tid = trials[0]["id"]
     base = f"http://127.0.0.1:{srv.port}"
+    views = ["#/experiments"] + [f"#/experiments/{eid}/{t}" for t in
+                                 ("overview", "trials", "hp", "compare", "checkpoints", "config", "code")] + \
+        [f"#/trials/{tid}", "#/runs", "#/projects", "#/projects/1", "#/jobs", "#/cluster", "#/tasks", "#/models",
+         "#/admin"]
     harness = """
 const els = {};
-function el(id) { return els[id] || (els[id] = {innerHTML: "", textContent: "", classList: {add() {}, remove() {}}, onclick: null}); }
+function el(id) { return els[id] || (els[id] = {innerHTML: "", textContent: "", scrollTop: 0, scrollHeight: 0,
+  classList: {add() {}, remove() {}, toggle() {}}, addEventListener() {}, onclick: null}); }
 global.document = {querySelector: s => el(s), querySelectorAll: () => []};
 global.localStorage = {getItem: () => "", setItem() {}};
-global.window = {};
+global.window = {DAMD_TEST: true};
 const http = require("http");
 global.fetch = (p, o) => new Promise((resolve, reject) => {  // node 12 has no fetch: a minimal one
   o = o || {};
@@ -97,18 +111,20 @@ global.fetch = (p, o) => new Promise((resolve, reject) => {  // node 12 has no f
   req.end();
 });
 global.location = {hash: "#/"};
-""".replace("BASE", json.dumps(base)) + js.replace("route().then(follow);", "") + """
+const app = require(APP);
 (async () => {
-  for (const h of ["#/", "#/exp/%d", "#/cluster", "#/models"]) {
-    location.hash = h; await route();
+  for (const h of VIEWS) {
+    location.hash = h; await app.route();
     if (els["#err"].textContent) { console.log("ERR " + h + " " + els["#err"].textContent); process.exit(1); }
     console.log("OK " + h + " " + els["#view"].innerHTML.length);
   }
 })();
-""" % eid
+""".replace("BASE", json.dumps(base)).replace("APP", json.dumps(str(ASSETS / "app.js"))).replace(
+        "VIEWS", json.dumps(views))
     f = tmp_path / "ui_test.js"
     f.write_text(harness)
-    out = subprocess.run(["node", str(f)], capture_output=True, text=True, timeout=60)
+    out = subprocess.run(["node", str(f)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
-    lines = out.stdout.split()
-    assert lines.count("OK") == 4, out.stdout
+    ok = [ln for ln in out.stdout.splitlines() if ln.startswith("OK ")]
+    assert len(ok) == len(views), out.stdout
+    assert all(int(ln.split()[-1]) > 100 for ln in ok), out.stdout  # every view rendered content
