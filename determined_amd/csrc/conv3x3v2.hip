@@ -54,6 +54,13 @@ __device__ __forceinline__ int a_row(int i, int rho) { return 32 * (i >> 1) + 8 
 // 16 bytes from rsrc + voff (per lane) + soff (wave-uniform) to LDS (buffer_load_dwordx4 ... lds).  Kept out
 // of the kernel's lambdas: an amdgcn builtin called directly inside them makes hipcc drop the host launch
 // stub of the kernel template (declared, never defined: an undefined symbol at load time)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// bf16 element `hi` (0: low half, 1: high half) of a packed dword, as float
+__device__ __forceinline__ float bf_lo(uint32_t d, int hi) {
+  return __uint_as_float(hi ? (d & 0xffff0000u) : (d << 16));
+}
+
 __device__ __forceinline__ void dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff, void* lds_dst) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, voff, soff, 0, 0);
 }
@@ -207,7 +214,9 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   };
 
   // ---- register-staged halo of one unit
-  bf16x8 hx[NCH], hy[PRO == 2 ? NCH : 1];
+  // native 4 x u32 vectors: a select / copy of an aggregate (bf16x8) made the compiler keep the
+  // array in scratch memory (private segment) for the PRO = 0 variants -- 2x slower
+  u32x4 hx[NCH], hy[PRO == 2 ? NCH : 1];
   int h_tile = 0, h_cb = 0;
   auto load_halo = [&](int u) __attribute__((always_inline)) {
     h_tile = unit_tile(u);
@@ -219,8 +228,8 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       const int hr = static_cast<int>(hmeta[i] >> 8);
       const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
       const int64_t off = ok ? base + hrel[i] : 0;  // clamped: zeroed at the store
-      hx[i] = *reinterpret_cast<const bf16x8*>(x + off);
-      if (PRO == 2) hy[i] = *reinterpret_cast<const bf16x8*>(pa.res + off);
+      hx[i] = *reinterpret_cast<const u32x4*>(x + off);
+      if (PRO == 2) hy[i] = *reinterpret_cast<const u32x4*>(pa.res + off);
     }
   };
   auto store_halo = [&](int buf) __attribute__((always_inline)) {
@@ -241,28 +250,29 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       if (!(hmeta[i] & 2u)) continue;  // beyond the halo (last round of chunks)
       const int hr = static_cast<int>(hmeta[i] >> 8);
       const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
-      bf16x8 o;
+      u32x4 o;
       if (PRO) {
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float t = PRO == 2 ? fs[e] * bf2f(hx[i].v[e]) + fr[e] * bf2f(hy[i].v[e]) + fh[e]
-                                   : fmaxf(bf2f(hx[i].v[e]) * fs[e] + fh[e], 0.f);
+          const float xv = bf_lo(hx[i][e >> 1], e & 1);
+          const float t = PRO == 2 ? fs[e] * xv + fr[e] * bf_lo(hy[i][e >> 1], e & 1) + fh[e]
+                                   : fmaxf(xv * fs[e] + fh[e], 0.f);
           v[e] = ok ? t : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           const u16v2_t pk = f2bf2(v[e], v[e + 1]);
-          o.v[e] = pk[0];
-          o.v[e + 1] = pk[1];
+          o[e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
         }
       } else {
-        o = ok ? hx[i] : bf16x8{};
+        const uint32_t keep = ok ? 0xffffffffu : 0u;  // per-dword mask: no aggregate select
+        o = hx[i] & keep;
       }
-      *reinterpret_cast<bf16x8*>(halo + buf * S::HB + hlds[i]) = o;
+      *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds[i]) = o;
       // the tile's own rows: the transformed operand is an output (weight gradient / BN backward)
       if (PRO && pa.aout != nullptr && ct == 0 && ok && hr >= 1 && hr <= TR)
-        *reinterpret_cast<bf16x8*>(pa.aout + tile_pix0 * g.C + hrel[i] + h_cb * kBK) = o;
+        *reinterpret_cast<u32x4*>(pa.aout + tile_pix0 * g.C + hrel[i] + h_cb * kBK) = o;
     }
   };
 
