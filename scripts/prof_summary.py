@@ -7,7 +7,7 @@ import sys
 def cat(n: str) -> str:
     if "damd::bn_" in n:
         return "bn(ours)"
-    if "damd::igemm" in n or "damd::stem" in n:
+    if "damd::igemm" in n or "damd::stem" in n or "damd::c3v2" in n:
         return "conv(ours)"
     if "damd::" in n:
         return "optim/norm(ours)"
