@@ -13,18 +13,22 @@
 //     the same for every tile and is computed once per launch;
 //   * the halo is a (TR + 2) x (W + 2) grid of slots with the image border as real zero slots, so no
 //     tap ever needs a validity test;
-//   * a slot is 144 bytes (64 channels + 16 pad bytes): 16 consecutive slots at the same 16-byte
-//     chunk hit 16 distinct bank quads (144 * s mod 256 is distinct for s mod 16), so the reads need
-//     no XOR swizzle; with W a template constant every tap / k-half offset is an immediate of the
-//     ds_read, and a B-fragment read costs no VALU instruction at all;
-//   * the lanes beyond TR * W pixels (W = 56 or 28 is 7 * 2^k: the 16-pixel fragments leave 1/8 of
-//     the lanes idle) read slot 0 and are never stored.
+//   * the halo is chunk-planar (16-byte channel chunk c of slot s at c * PLANE + 16 s) and the pixel
+//     lanes are row-padded (W -> multiple of 16), so a fragment's 16 lanes read 16 consecutive slots of
+//     one image row: the ds_read_b128 lane groups, which mix two chunks (lanes {0-3, 12-15} and {20-27}),
+//     hit 16 distinct bank quads with no swizzle.  (The first version -- 144-byte pixel slots, 8 waves --
+//     spent 23% of its LDS cycles in bank conflicts: profiles/conv3x3v2_pmc_*.)  With W a template
+//     constant every tap / k-half offset is an immediate of the ds_read: a B-fragment read costs no VALU;
+//   * 4 waves, each a 64-channel x 64-pixel tile: 16 MFMAs per 4 + 4 fragment reads, half the LDS read
+//     traffic per MFMA of 8 waves with 32-pixel tiles (which re-read every weight fragment 8 times and
+//     kept the LDS array ~75% busy); one wave per SIMD with the whole 512-register file, the next tap's
+//     fragments prefetched while the current tap's 32 MFMAs run.
 // The halo is register-staged (global_load_dwordx4 -> optional BN transform -> ds_write_b128), loaded
 // at the first tap of a 64-channel unit and written into the other halo buffer at tap 4, so it
-// overlaps the unit's MFMAs; weights stream per tap through a 3-slot LDS ring filled by the buffer
-// LDS-DMA (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
-// Work split: persistent blocks (one per CU, 8 waves), each a contiguous run of tiles, so consecutive
-// tiles of an image -- which share two halo rows -- run back to back on the same CU / XCD L2.
+// overlaps the unit's MFMAs; weights stream per tap through a 5-slot LDS ring filled 4 taps ahead by the
+// buffer LDS-DMA (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
+// Work split: persistent blocks (one per CU), each a contiguous run of tiles, so consecutive tiles of an
+// image -- which share two halo rows -- run back to back on the same CU / XCD L2.
 
 #include <cstdlib>
 
@@ -39,7 +43,6 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kBK = 64;      // channels per unit (one k-step of 64 per tap)
-constexpr int kSlotB = 144;  // bytes per halo slot
 
 constexpr int kEpiNone = 0, kEpiStats = 1, kEpiBnbM = 2, kEpiBnbR = 3;  // conv_igemm.hip EPI modes
 
@@ -95,24 +98,34 @@ struct ProArgs {
   bf16_t* aout;          // the transformed operand [M][C] (tile rows only), or null
 };
 
-// TR image rows x W pixels per tile; BCO output channels per block; WCO co-waves x (NW / WCO) pixel waves
+// TR image rows x W pixels per tile; BCO output channels per block; WCO co-waves x (NW / WCO) pixel waves.
+// Halo layout (chunk-planar): the 16-byte channel chunk c (channels 8c .. 8c + 7 of the unit) of halo slot
+// s is at c * PLANE + 16 * s.  A 16-lane fragment row covers 16 consecutive slots of ONE image row (the
+// pixel lanes are row-padded to WR = W rounded up to 16), and the ds_read_b128 lane groups
+// ({0-3, 12-15 | 20-27}, ...) mix two chunks of 8 + 8 slots: with PLANE a multiple of 256 bytes the 16
+// addresses of a group always fall in 16 distinct bank quads -- no swizzle, no conflict.
 template <int W, int TR, int BCO, int WCO, int NW>
 struct Shape {
-  static constexpr int WP = W + 2;                      // padded row
-  static constexpr int HS = (TR + 2) * WP;              // halo slots
-  static constexpr int HB = (HS * kSlotB + 255) / 256 * 256;  // halo buffer bytes
-  static constexpr int P = TR * W;                      // real pixels per tile
-  static constexpr int PW = NW / WCO;                   // pixel waves
-  static constexpr int PL = (P + 16 * PW - 1) / (16 * PW) * (16 * PW);  // pixel lanes (>= P)
+  static constexpr int RS = W + 2;                        // slots per halo row (zero column at both ends)
+  static constexpr int HS = (TR + 2) * RS;                // halo slots
+  static constexpr int WR = (W + 15) / 16 * 16;           // pixel lanes per image row
+  static constexpr int XS = WR + 2 > RS ? WR + 2 - RS : 0;  // slots past HS that idle lanes read
+  static constexpr int PLANE = ((HS + XS) * 16 + 255) / 256 * 256;
+  static constexpr int HB = 8 * PLANE;                    // halo buffer bytes (64 channels)
+  static constexpr int P = TR * WR;                       // lane pixels per tile (row-padded)
+  static constexpr int PW = NW / WCO;                     // pixel waves
+  static constexpr int PL = (P + 16 * PW - 1) / (16 * PW) * (16 * PW);
   static constexpr int TP = PL / PW, TCO = BCO / WCO;
   static constexpr int FI = TCO / 16, FJ = TP / 16;
   static constexpr int NT = 64 * NW;
-  static constexpr int NCH = (HS * 8 + NT - 1) / NT;    // halo 16-byte chunks per thread
-  static constexpr int NIW = BCO / (8 * NW);            // weight DMA instructions per wave per tap
-  static constexpr int WSLOT = BCO * kBK * 2;           // bytes per weight ring slot
-  static constexpr int LDS = 2 * HB + 3 * WSLOT + 3 * BCO * 4;
+  static constexpr int NCH = (HS * 8 + NT - 1) / NT;      // halo 16-byte chunks per thread
+  static constexpr int NIW = BCO / (8 * NW);              // weight DMA instructions per wave per tap
+  static constexpr int WSLOT = BCO * kBK * 2;             // bytes per weight ring slot
+  static constexpr int RING = 5;                          // weight ring slots (DMA 4 taps ahead)
+  static constexpr int LDS = 2 * HB + RING * WSLOT + 3 * BCO * 4;
   static_assert(FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && WCO * PW == NW, "bad tile");
-  static_assert(NCH <= 8, "halo chunks per thread");
+  static_assert(NT % 128 == 0 && NCH <= 16, "halo staging map");
+  static_assert(4 * PLANE + ((2 * RS + 2) * 16) < 65536, "ds_read immediate offsets");
 };
 
 template <int W, int TR, int BCO, int WCO, int NW, int EPI, int PRO>
@@ -120,13 +133,13 @@ __global__ void __launch_bounds__(64 * NW, 1)
 conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                  float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
   using S = Shape<W, TR, BCO, WCO, NW>;
-  constexpr int FI = S::FI, FJ = S::FJ, NT = S::NT, NCH = S::NCH, NIW = S::NIW;
+  constexpr int FI = S::FI, FJ = S::FJ, NT = S::NT, NCH = S::NCH, NIW = S::NIW, RING = S::RING;
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int LPC = PRO == 2 ? 2 : 1;  // global loads per halo chunk
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* halo = lds;                             // [2][HB]
-  char* wts = lds + 2 * S::HB;                  // [3][BCO][64] bf16, swizzled
-  float* prm = reinterpret_cast<float*>(wts + 3 * S::WSLOT);  // [3][BCO]: mean, scale, shift
+  char* wts = lds + 2 * S::HB;                  // [RING][BCO][64] bf16, swizzled
+  float* prm = reinterpret_cast<float*>(wts + RING * S::WSLOT);  // [3][BCO]: mean, scale, shift
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -141,6 +154,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   const int t_begin = static_cast<int>(static_cast<int64_t>(grp) * g.ntiles / g.groups);
   const int t_end = static_cast<int>(static_cast<int64_t>(grp + 1) * g.ntiles / g.groups);
   const int units = (t_end - t_begin) * g.cblk;
+  const int nitems = units * 9;
   const int tiles_per_img = g.H / TR;
 
   if (EPI >= kEpiBnbM) {
@@ -152,31 +166,33 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
     }
   }
 
-  // ---- halo staging roles (tile-invariant): chunk u = tid + NT * i -> slot u / 8, channel chunk u % 8
-  // (= tid % 8 for every i); relative input offset of the slot's pixel from the tile's first pixel
-  const int hc = tid & 7;
-  int32_t hrel[NCH];     // elements (may be negative); only used when the slot is inside the image
+  // ---- halo staging roles (tile-invariant): chunk u = tid + NT * i -> channel chunk hc = (u >> 4) & 7 (the
+  // same for every i), slot (u & 15) + 16 * (u >> 7): 16 consecutive lanes write 16 consecutive slots
+  const int hc = (tid >> 4) & 7;
+  int32_t hrel[NCH];     // input offset (elements) of the slot's pixel from the tile's first pixel
   uint32_t hlds[NCH];    // byte offset of the chunk in a halo buffer
-  uint32_t hmeta[NCH];   // bit 0: chunk exists and is inside the image columns; bits 8..: padded row hr
+  uint32_t hmeta[NCH];   // bit 0: inside the image columns; bit 1: a halo slot; bits 8..: halo row
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    const int u = tid + NT * i, slot = u >> 3;
-    const int hr = slot / S::WP, wc = slot - (slot / S::WP) * S::WP;
-    const bool ok = u < S::HS * 8 && wc >= 1 && wc <= W;
+    const int u = tid + NT * i, slot = (u & 15) + 16 * (u >> 7);
+    const int hr = slot / S::RS, wc = slot - (slot / S::RS) * S::RS;
+    const bool in = slot < S::HS;
+    const bool ok = in && wc >= 1 && wc <= W;
     hrel[i] = ((hr - 1) * W + (wc - 1)) * g.C + hc * 8;
-    hlds[i] = static_cast<uint32_t>(slot * kSlotB + hc * 16);
-    hmeta[i] = (ok ? 1u : 0u) | (static_cast<uint32_t>(hr) << 8) | ((u < S::HS * 8 ? 1u : 0u) << 1);
+    hlds[i] = static_cast<uint32_t>(hc * S::PLANE + slot * 16);
+    hmeta[i] = (ok ? 1u : 0u) | ((in ? 1u : 0u) << 1) | (static_cast<uint32_t>(hr) << 8);
   }
-  // ---- B-fragment bases: lane's pixel p = wp0 + 16 j + rho -> slot of tap (0, 0) = (p / W) * WP + p % W
+  // ---- B-fragment bases: lane pixel p = wp0 + 16 j + rho = (image row p / WR, column p % WR) -> slot of
+  // tap (0, 0) = row * RS + column; chunk lg of k-half 0 (k-half 1: + 4 planes, an immediate)
   uint32_t bb[2][FJ];
 #pragma unroll
   for (int j = 0; j < FJ; ++j) {
     const int p = wp0 + 16 * j + rho;
-    const int s0 = p < S::P ? (p / W) * S::WP + (p - (p / W) * W) : 0;
-    bb[0][j] = static_cast<uint32_t>(s0 * kSlotB + lg * 16);
+    const int s0 = p < S::P ? (p / S::WR) * S::RS + (p - (p / S::WR) * S::WR) : 0;
+    bb[0][j] = static_cast<uint32_t>(s0 * 16 + lg * S::PLANE);
     bb[1][j] = bb[0][j] + S::HB;
   }
-  // ---- A-fragment (weight) offsets of ring slot 0; slots are immediates
+  // ---- A-fragment (weight) offsets in ring slot 0 (+ slot * WSLOT per item)
   const uint32_t wts_b = 2u * S::HB;
   uint32_t aoff[2][FI];
 #pragma unroll
@@ -198,24 +214,25 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   const __amdgpu_buffer_rsrc_t rs_w =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(w), 0, static_cast<int>(g.wbytes), 0x00020000);
 
-  // unit index -> (tile, channel block); tile -> image n, first row h0
   auto unit_tile = [&](int u) __attribute__((always_inline)) { return t_begin + u / g.cblk; };
   auto unit_cb = [&](int u) __attribute__((always_inline)) { return u - (u / g.cblk) * g.cblk; };
 
-  // weight items: item = unit * 9 + tap; DMA into ring slot item % 3
-  auto issue_w = [&](int item, int rslot) __attribute__((always_inline)) {
-    const int u = item / 9, tap = item - (item / 9) * 9;
-    const int cb = unit_cb(u);
-    const int soff = (tap * g.C + cb * kBK) * 2;  // wave-uniform
-    char* dst = wts + rslot * S::WSLOT;
+  // weight item = unit * 9 + tap, DMA'd into ring slot item % RING; soff: the tap's and channel block's
+  // byte offset in a weight row (wave-uniform)
+  auto issue_w = [&](int soff, int slot) __attribute__((always_inline)) {
+    char* dst = wts + slot * S::WSLOT;
 #pragma unroll
     for (int i = 0; i < NIW; ++i)
       dma16b(rs_w, wvoff[i], soff, dst + 8 * (wave + NW * i) * kBK * 2);
   };
+  auto ring = [](int s0, int k) __attribute__((always_inline)) {  // (s0 + k) % RING for s0 < RING, k < 3 RING
+    int r = s0 + k;
+    r = r >= 2 * RING ? r - 2 * RING : r;
+    return r >= RING ? r - RING : r;
+  };
+  static_assert(8 + RING - 1 + RING - 1 < 4 * RING, "ring(): slot + tap lookahead range");
 
-  // ---- register-staged halo of one unit
-  // native 4 x u32 vectors: a select / copy of an aggregate (bf16x8) made the compiler keep the
-  // array in scratch memory (private segment) for the PRO = 0 variants -- 2x slower
+  // ---- register-staged halo of one unit (native vectors: an aggregate select would go to scratch)
   u32x4 hx[NCH], hy[PRO == 2 ? NCH : 1];
   int h_tile = 0, h_cb = 0;
   auto load_halo = [&](int u) __attribute__((always_inline)) {
@@ -266,7 +283,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
           o[e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
         }
       } else {
-        const uint32_t keep = ok ? 0xffffffffu : 0u;  // per-dword mask: no aggregate select
+        const uint32_t keep = ok ? 0xffffffffu : 0u;
         o = hx[i] & keep;
       }
       *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds[i]) = o;
@@ -287,22 +304,23 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 #pragma unroll
     for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
 
-  // ---- epilogue of one tile: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of pixel p_j
+  // ---- epilogue of one tile: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of lane pixel p_j
   auto epilogue = [&](int tile) __attribute__((always_inline)) {
     const int n = tile / tiles_per_img, h0 = (tile - n * tiles_per_img) * TR;
     const int64_t m0 = (static_cast<int64_t>(n) * g.H + h0) * W;
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const int p = wp0 + 16 * j + rho;
-      const bool okp = p < S::P;
-      const int64_t m = m0 + (okp ? p : 0);
-      bf16x8 yr[FI / 2];
+      const int pr = p / S::WR, pc = p - (p / S::WR) * S::WR;
+      const bool okp = p < S::P && pc < W;
+      const int64_t m = m0 + (okp ? pr * W + pc : 0);
+      u32x4 yr[FI / 2];
       uint32_t mb[FI / 2];
       if (EPI >= kEpiBnbM) {
 #pragma unroll
         for (int q = 0; q < FI / 2; ++q) {
           const int64_t off = m * g.K + static_cast<int64_t>(ct) * BCO + wco0 + 32 * q + 8 * lg;
-          yr[q] = *reinterpret_cast<const bf16x8*>(ea.yb + off);
+          yr[q] = *reinterpret_cast<const u32x4*>(ea.yb + off);
           if (EPI == kEpiBnbM) mb[q] = ea.mask[off >> 3];
         }
       }
@@ -315,7 +333,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
         float yv[8];
         if (EPI >= kEpiBnbM) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) yv[e] = bf2f(yr[q].v[e]);
+          for (int e = 0; e < 8; ++e) yv[e] = bf_lo(yr[q][e >> 1], e & 1);
           if (EPI == kEpiBnbM) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = (mb[q] >> e) & 1u ? o[e] : 0.f;
@@ -324,15 +342,14 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
             for (int e = 0; e < 8; ++e) o[e] = yv[e] * prm[BCO + cl + e] + prm[2 * BCO + cl + e] > 0.f ? o[e] : 0.f;
           }
         }
-        bf16x8 v;
+        u32x4 v;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           const u16v2_t pk = f2bf2(o[e], o[e + 1]);
-          v.v[e] = pk[0];
-          v.v[e + 1] = pk[1];
+          v[e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
         }
         if (okp) {
-          *reinterpret_cast<bf16x8*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + cl) = v;
+          *reinterpret_cast<u32x4*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + cl) = v;
           if (EPI == kEpiStats) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -342,7 +359,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
           } else if (EPI >= kEpiBnbM) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float f = bf2f(v.v[e]);
+              const float f = bf_lo(v[e >> 1], e & 1);
               st_s[q][e] += f;
               st_q[q][e] += f * (yv[e] - prm[cl + e]);
             }
@@ -359,59 +376,91 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   const char* lds_c = lds;
   auto ld = [&](uint32_t off) __attribute__((always_inline)) { return *reinterpret_cast<const s8*>(lds_c + off); };
 
-  // ---- prologue: unit 0's halo into buffer 0, weight items 0 and 1 in flight
+  // fragment double buffer: set P holds the operands of the item being multiplied, set P ^ 1 is being
+  // prefetched for the next item (P = item parity, compile-time inside the 18-tap unroll)
+  s8 fa[2][2][FI], fb[2][2][FJ];
+  // load the fragments of an item (tap T, halo buffer B: compile-time; its weights in ring slot `slot`) into
+  // set SET
+  auto fetch = [&](auto TT, auto BUF, auto SET, int slot) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value, SE = decltype(SET)::value;
+    constexpr uint32_t toff = static_cast<uint32_t>(((T / 3) * S::RS + (T % 3)) * 16);
+    const uint32_t roff = static_cast<uint32_t>(slot * S::WSLOT);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i) fa[SE][kk][i] = ld(aoff[kk][i] + roff);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) fb[SE][kk][j] = ld(bb[B][j] + toff + kk * 4 * S::PLANE);
+    }
+  };
+
+  // ---- prologue: unit 0's halo into buffer 0, weight items 0 .. 3 in flight, item 0's fragments
   if (units > 0) {
     load_halo(0);
     store_halo(0);
-    issue_w(0, 0);
-    issue_w(1, 1);
+    const int cb0 = unit_cb(0), cb1 = units > 1 ? unit_cb(1) : 0;
+#pragma unroll
+    for (int it = 0; it < RING - 1; ++it)
+      if (it < nitems) issue_w(((it < 9 ? it : it - 9) * g.C + (it < 9 ? cb0 : cb1) * kBK) * 2, it);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    fetch(IC<0>{}, IC<0>{}, IC<0>{}, 0);
   }
-  const int nitems = units * 9;
 
-  // one tap: item it = u * 9 + T (T compile-time: ring slot T % 3 and the tap's row / column shift are
-  // immediates); HB_: halo buffer of unit u (0 / 1, compile-time via the two-unit unroll)
-  auto tap = [&](auto TT, auto BUF, int u, int it) __attribute__((always_inline)) {
-    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value;
-    // the weights of item it landed: younger are item it+1's DMA and, at T = 1, the halo loads issued
-    // at T = 0 (after item it+1's DMA was issued at the previous item)
-    if (it + 1 < nitems) {
-      if (T == 1 && u + 1 < units) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW + NCH * LPC) : "memory");
+  // one tap: item it = u * 9 + T; operands in set SE (loaded during the previous tap).  rs0: ring slot of
+  // item u * 9; wo_u / wo_n: channel-block byte offsets of units u and u + 1 in a weight row
+  auto tap = [&](auto TT, auto BUF, auto SET, int u, int it, int rs0, int wo_u, int wo_n)
+      __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value, SE = decltype(SET)::value;
+    // item it+1's weights landed (own DMA; the barrier makes every wave's visible).  Younger VMEM ops:
+    // the DMAs of items it+2, it+3 and, at T = 1..3, the next unit's halo loads issued at T = 0
+    const bool hl = (T >= 1 && T <= 3) && u + 1 < units;
+    if (it + 3 < nitems) {
+      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW + NCH * LPC) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW) : "memory");
+    } else if (it + 2 < nitems) {
+      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW + NCH * LPC) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's halo stores / last reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own halo stores and this item's fragments
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (it + RING - 1 < nitems) {  // item it+4: its slot last held item it-1 (read before the barrier)
+      constexpr int TN = T + RING - 1;
+      issue_w(TN < 9 ? TN * 2 * g.C + wo_u : (TN - 9) * 2 * g.C + wo_n, ring(rs0, TN));
+    }
     if (T == 0 && u + 1 < units) load_halo(u + 1);
-    if (it + 2 < nitems) issue_w(it + 2, (T + 2) % 3);
     if (T == 4 && u + 1 < units) store_halo(B ^ 1);  // buffer B^1 was last read by unit u-1
-    constexpr uint32_t toff = static_cast<uint32_t>(((T / 3) * S::WP + (T % 3)) * kSlotB);
-    constexpr uint32_t roff = static_cast<uint32_t>((T % 3) * S::WSLOT);
+    // prefetch the next item's operands (tap T+1, or tap 0 of unit u+1 in the other halo buffer)
+    if (it + 1 < nitems) {
+      if constexpr (T < 8) fetch(IC<T + 1>{}, IC<B>{}, IC<SE ^ 1>{}, ring(rs0, T + 1));
+      else fetch(IC<0>{}, IC<B ^ 1>{}, IC<SE ^ 1>{}, ring(rs0, T + 1));
+    }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      s8 a[FI], b[FJ];
-#pragma unroll
-      for (int i = 0; i < FI; ++i) a[i] = ld(aoff[kk][i] + roff);
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) b[j] = ld(bb[B][j] + toff + kk * 64);
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
-    }
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[SE][kk][i], fb[SE][kk][j], acc[i][j]);
   };
   auto unit_body = [&](auto BUF, int u) __attribute__((always_inline)) {
+    constexpr int B = decltype(BUF)::value;  // = u & 1 = parity of the unit's first item (9u even iff u even)
     const int it = u * 9;
-    tap(IC<0>{}, BUF, u, it);
-    tap(IC<1>{}, BUF, u, it + 1);
-    tap(IC<2>{}, BUF, u, it + 2);
-    tap(IC<3>{}, BUF, u, it + 3);
-    tap(IC<4>{}, BUF, u, it + 4);
-    tap(IC<5>{}, BUF, u, it + 5);
-    tap(IC<6>{}, BUF, u, it + 6);
-    tap(IC<7>{}, BUF, u, it + 7);
-    tap(IC<8>{}, BUF, u, it + 8);
+    const int rs0 = it % RING;
+    const int wo_u = unit_cb(u) * kBK * 2, wo_n = u + 1 < units ? unit_cb(u + 1) * kBK * 2 : 0;
+    tap(IC<0>{}, BUF, IC<B>{}, u, it, rs0, wo_u, wo_n);
+    tap(IC<1>{}, BUF, IC<B ^ 1>{}, u, it + 1, rs0, wo_u, wo_n);
+    tap(IC<2>{}, BUF, IC<B>{}, u, it + 2, rs0, wo_u, wo_n);
+    tap(IC<3>{}, BUF, IC<B ^ 1>{}, u, it + 3, rs0, wo_u, wo_n);
+    tap(IC<4>{}, BUF, IC<B>{}, u, it + 4, rs0, wo_u, wo_n);
+    tap(IC<5>{}, BUF, IC<B ^ 1>{}, u, it + 5, rs0, wo_u, wo_n);
+    tap(IC<6>{}, BUF, IC<B>{}, u, it + 6, rs0, wo_u, wo_n);
+    tap(IC<7>{}, BUF, IC<B ^ 1>{}, u, it + 7, rs0, wo_u, wo_n);
+    tap(IC<8>{}, BUF, IC<B>{}, u, it + 8, rs0, wo_u, wo_n);
     if (unit_cb(u) == g.cblk - 1) epilogue(unit_tile(u));
   };
   for (int u = 0; u < units; u += 2) {
@@ -458,9 +507,10 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 struct V2Cfg {
   int W, TR, bco, wco, nw;
 };
-// 0: 56x56 layers (64 channels), 4-row tiles; 1: 28x28 layers (128 channels), 4-row tiles;
-// 2: 14x14 layers, one image per tile (196 of 256 lanes used)
-constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 8}, {28, 4, 128, 2, 8}, {14, 14, 128, 2, 8}};
+// 4 waves, each a 64-channel x 64-pixel tile (16 MFMAs per 4 + 4 fragment reads):
+// 0: 56x56 layers, 4-row tiles (64 co); 1: 28x28 layers, 4-row tiles (128 co, 2 co-waves);
+// 2: 14x14 layers, one image per tile (64 co)
+constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 4}, {28, 4, 128, 2, 4}, {14, 14, 64, 1, 4}};
 constexpr int kNumV2 = sizeof(kV2) / sizeof(kV2[0]);
 
 template <int W, int TR, int BCO, int WCO, int NW>
@@ -470,9 +520,9 @@ int lds_bytes() {
 
 int v2_lds(int cfg) {
   switch (cfg) {
-    case 0: return lds_bytes<56, 4, 64, 1, 8>();
-    case 1: return lds_bytes<28, 4, 128, 2, 8>();
-    default: return lds_bytes<14, 14, 128, 2, 8>();
+    case 0: return lds_bytes<56, 4, 64, 1, 4>();
+    case 1: return lds_bytes<28, 4, 128, 2, 4>();
+    default: return lds_bytes<14, 14, 64, 1, 4>();
   }
 }
 
@@ -558,9 +608,9 @@ int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, in
     else return -4;                                                                                          \
   } while (0)
   switch (cfg) {
-    case 0: V2E(56, 4, 64, 1, 8); break;
-    case 1: V2E(28, 4, 128, 2, 8); break;
-    default: V2E(14, 14, 128, 2, 8); break;
+    case 0: V2E(56, 4, 64, 1, 4); break;
+    case 1: V2E(28, 4, 128, 2, 4); break;
+    default: V2E(14, 14, 64, 1, 4); break;
   }
 #undef V2E
 #undef V2L

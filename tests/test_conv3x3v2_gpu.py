@@ -31,9 +31,10 @@ def _rand(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16).contiguous(memory_format=CL)
 
 
-# (n, cin, cout, H, W): one v2 config each plus multi channel-block / co-tile and non-square cases
+# (n, cin, cout, H, W): one v2 config each plus multi channel-block (cin / 64 = 2, 3, 4: the weight ring
+# wraps at different taps per unit) / co-tile and non-square cases
 SHAPES = [(2, 64, 64, 56, 56), (1, 128, 128, 8, 56), (3, 128, 128, 28, 28), (2, 64, 256, 12, 28),
-          (3, 128, 128, 14, 14), (2, 256, 256, 14, 14)]
+          (3, 128, 128, 14, 14), (2, 256, 256, 14, 14), (1, 256, 64, 4, 56), (2, 192, 128, 8, 28)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)

@@ -107,3 +107,29 @@ def test_model_hub_base_transformer_trial_local():
 
     out = expand_like([np.ones((2, 3)), np.ones((1, 5))])
     assert out.shape == (3, 5) and out[2, 4] == 1 and out[0, 4] == -100
+
+
+def test_accelerate_keeps_the_model_function():
+    """determined_amd.transformers.accelerate swaps attention / residual-LayerNorm for the fused
+    kernels; on CPU (fallback paths) the model computes the same logits, padding mask included, and
+    keeps its parameter names (checkpoints stay interchangeable with the stock model)."""
+    import copy
+
+    import torch
+
+    from determined_amd.ops.norm import FusedLayerNorm
+    from determined_amd.transformers import accelerate
+
+    cfg = transformers.BertConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=2, intermediate_size=128,
+                                  vocab_size=500)
+    torch.manual_seed(0)
+    stock = transformers.BertForMaskedLM(cfg).eval()
+    fused = accelerate(copy.deepcopy(stock)).eval()
+    assert fused.config._attn_implementation == "damd"
+    assert sum(isinstance(m, FusedLayerNorm) for m in fused.modules()) == 2 * 2 + 2
+    assert [n for n, _ in fused.named_parameters()] == [n for n, _ in stock.named_parameters()]
+    ids = torch.randint(0, 500, (3, 20))
+    am = torch.ones(3, 20, dtype=torch.long)
+    am[1, 13:] = 0
+    torch.testing.assert_close(fused(input_ids=ids, attention_mask=am).logits,
+                               stock(input_ids=ids, attention_mask=am).logits, rtol=1e-4, atol=1e-4)
