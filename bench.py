@@ -59,7 +59,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-pretune", action="store_true",
                    help="pick conv kernels inside the first warm-up step instead of a separate no-sync pass")
     # MIOpen immediate mode takes the solvers recorded in the in-tree find-db (searched once on an
-    # MI355X, scripts/gpu_finddb.sh) without re-running the search on every fresh box: batch 2048
+    # MI355X, scripts/archive/gpu_finddb.sh) without re-running the search on every fresh box: batch 2048
     # starts in ~11 s instead of ~300 s at the same throughput (15,957 / 15,980 vs 15,910 / 15,957
     # samples/s, profiles/resnet50_b2048_finddb_vs_immediate_1gpu.txt)
     p.add_argument("--conv-benchmark", type=int, default=0,

@@ -1547,6 +1547,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_bnact_fwd", &conv_bnact_fwd);
   m.def("conv_pro_supported", &conv_pro_supported);
   m.def("conv_num_cfgs", &conv_num_cfgs_all);
+  m.def("conv_v2_num_cfgs", &damd_v2_num_cfgs);  // the last conv_v2_num_cfgs() conv cfgs are conv3x3v2.hip's
   m.def("wgrad3x3_supported", &wgrad3x3_supported);
   m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported);
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);

@@ -19,14 +19,17 @@
 //     hit 16 distinct bank quads with no swizzle.  (The first version -- 144-byte pixel slots, 8 waves --
 //     spent 23% of its LDS cycles in bank conflicts: profiles/conv3x3v2_pmc_*.)  With W a template
 //     constant every tap / k-half offset is an immediate of the ds_read: a B-fragment read costs no VALU;
-//   * 4 waves, each a 64-channel x 64-pixel tile: 16 MFMAs per 4 + 4 fragment reads, half the LDS read
-//     traffic per MFMA of 8 waves with 32-pixel tiles (which re-read every weight fragment 8 times and
-//     kept the LDS array ~75% busy); one wave per SIMD with the whole 512-register file, the next tap's
-//     fragments prefetched while the current tap's 32 MFMAs run.
-// The halo is register-staged (global_load_dwordx4 -> optional BN transform -> ds_write_b128), loaded
-// at the first tap of a 64-channel unit and written into the other halo buffer at tap 4, so it
-// overlaps the unit's MFMAs; weights stream per tap through a 5-slot LDS ring filled 4 taps ahead by the
-// buffer LDS-DMA (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
+//   * 8 waves, 2 per SIMD (256 registers each), every wave a 64-channel x 32- or 64-pixel tile; a tap's
+//     fragments are read after its barrier into one register set, and the other wave on the SIMD
+//     multiplies while this one waits.  (A 4-wave variant -- 1 wave per SIMD, 64x64 wave tiles, fragments
+//     double-buffered across taps -- halved the LDS reads per MFMA but left the halo staging and epilogue
+//     VALU with no other wave to hide under: 3.4 VALU per MFMA, slower on every layer,
+//     profiles/conv3x3v2_4wave_vs_8wave_b2048_1gpu.txt.)
+// The halo is register-staged (global_load_dwordx4 -> optional BN transform -> ds_write_b128): loaded at
+// the first tap of a 64-channel unit and written into the other halo buffer at tap 5, so five taps of MFMAs
+// cover the HBM latency; the BN prologue's per-channel coefficients are staged in LDS once per launch.
+// Weights stream per tap through a 5-slot LDS ring filled 4 taps ahead by the buffer LDS-DMA
+// (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
 // Work split: persistent blocks (one per CU), each a contiguous run of tiles, so consecutive tiles of an
 // image -- which share two halo rows -- run back to back on the same CU / XCD L2.
 
@@ -98,14 +101,16 @@ struct ProArgs {
   bf16_t* aout;          // the transformed operand [M][C] (tile rows only), or null
 };
 
-// TR image rows x W pixels per tile; BCO output channels per block; WCO co-waves x (NW / WCO) pixel waves.
+// TR image rows x W pixels per tile; BCO output channels per block; 8 waves = WCO co-waves x (8 / WCO) pixel
+// waves; NB halo buffers (2: the next unit's halo is written during this unit's taps; 1: between units).
 // Halo layout (chunk-planar): the 16-byte channel chunk c (channels 8c .. 8c + 7 of the unit) of halo slot
 // s is at c * PLANE + 16 * s.  A 16-lane fragment row covers 16 consecutive slots of ONE image row (the
 // pixel lanes are row-padded to WR = W rounded up to 16), and the ds_read_b128 lane groups
 // ({0-3, 12-15 | 20-27}, ...) mix two chunks of 8 + 8 slots: with PLANE a multiple of 256 bytes the 16
 // addresses of a group always fall in 16 distinct bank quads -- no swizzle, no conflict.
-template <int W, int TR, int BCO, int WCO, int NW>
+template <int W, int TR, int BCO, int WCO, int NB>
 struct Shape {
+  static constexpr int NW = 8;
   static constexpr int RS = W + 2;                        // slots per halo row (zero column at both ends)
   static constexpr int HS = (TR + 2) * RS;                // halo slots
   static constexpr int WR = (W + 15) / 16 * 16;           // pixel lanes per image row
@@ -122,24 +127,26 @@ struct Shape {
   static constexpr int NIW = BCO / (8 * NW);              // weight DMA instructions per wave per tap
   static constexpr int WSLOT = BCO * kBK * 2;             // bytes per weight ring slot
   static constexpr int RING = 5;                          // weight ring slots (DMA 4 taps ahead)
-  static constexpr int LDS = 2 * HB + RING * WSLOT + 3 * BCO * 4;
-  static_assert(FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && WCO * PW == NW, "bad tile");
+  static constexpr int LDS = NB * HB + RING * WSLOT + 3 * BCO * 4;  // + the PRO coefficients [2 or 3][C] fp32
+  static_assert(FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && WCO * PW == NW && (NB == 1 || NB == 2), "bad tile");
   static_assert(NT % 128 == 0 && NCH <= 16, "halo staging map");
   static_assert(4 * PLANE + ((2 * RS + 2) * 16) < 65536, "ds_read immediate offsets");
 };
 
-template <int W, int TR, int BCO, int WCO, int NW, int EPI, int PRO>
-__global__ void __launch_bounds__(64 * NW, 1)
+template <int W, int TR, int BCO, int WCO, int NB, int EPI, int PRO>
+__global__ void __launch_bounds__(512, 1)
 conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                  float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
-  using S = Shape<W, TR, BCO, WCO, NW>;
+  using S = Shape<W, TR, BCO, WCO, NB>;
+  constexpr int NW = S::NW;
   constexpr int FI = S::FI, FJ = S::FJ, NT = S::NT, NCH = S::NCH, NIW = S::NIW, RING = S::RING;
   constexpr bool SUMS = EPI != kEpiNone;
   constexpr int LPC = PRO == 2 ? 2 : 1;  // global loads per halo chunk
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* halo = lds;                             // [2][HB]
-  char* wts = lds + 2 * S::HB;                  // [RING][BCO][64] bf16, swizzled
+  char* halo = lds;                             // [NB][HB]
+  char* wts = lds + NB * S::HB;                 // [RING][BCO][64] bf16, swizzled
   float* prm = reinterpret_cast<float*>(wts + RING * S::WSLOT);  // [3][BCO]: mean, scale, shift
+  float* ppar = reinterpret_cast<float*>(lds + S::LDS);           // PRO: [3][C] scale, shift, rscale
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -165,22 +172,61 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       prm[2 * BCO + t] = EPI == kEpiBnbR ? ea.shift[co] : 0.f;
     }
   }
+  if (PRO) {
+    for (int t = tid; t < g.C; t += NT) {
+      ppar[t] = pa.scale[t];
+      ppar[g.C + t] = pa.shift[t];
+      if (PRO == 2) ppar[2 * g.C + t] = pa.rscale[t];
+    }
+  }
 
   // ---- halo staging roles (tile-invariant): chunk u = tid + NT * i -> channel chunk hc = (u >> 4) & 7 (the
   // same for every i), slot (u & 15) + 16 * (u >> 7): 16 consecutive lanes write 16 consecutive slots
+  // Loads are buffer loads from a per-unit resource based at halo slot 0's pixel (image row h0 - 1, column
+  // -1): a chunk's byte offset hoff is the same for every unit, and a chunk outside the image gets offset
+  // 2^31, past the resource's range, which the hardware answers with zeros -- no address arithmetic or
+  // zero-select per chunk.
   const int hc = (tid >> 4) & 7;
-  int32_t hrel[NCH];     // input offset (elements) of the slot's pixel from the tile's first pixel
-  uint32_t hlds[NCH];    // byte offset of the chunk in a halo buffer
-  uint32_t hmeta[NCH];   // bit 0: inside the image columns; bit 1: a halo slot; bits 8..: halo row
+  uint32_t hoff[NCH];    // byte offset of the chunk from halo slot 0's pixel, channel block 0
+  uint32_t ok_s = 0, top_m = 0, bot_m = 0, in_m = 0;  // bit i: chunk i inside the image columns / in halo
+                                                      // row 0 / in halo row TR + 1 / a halo slot at all
+  // chunk i's slot is slot0 + 2 NT / 16 * i: its LDS offset is hlds0 + 2 NT * i (an immediate)
+  const uint32_t hlds0 = static_cast<uint32_t>(hc * S::PLANE + ((tid & 15) + 16 * (tid >> 7)) * 16);
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int u = tid + NT * i, slot = (u & 15) + 16 * (u >> 7);
     const int hr = slot / S::RS, wc = slot - (slot / S::RS) * S::RS;
     const bool in = slot < S::HS;
     const bool ok = in && wc >= 1 && wc <= W;
-    hrel[i] = ((hr - 1) * W + (wc - 1)) * g.C + hc * 8;
-    hlds[i] = static_cast<uint32_t>(hc * S::PLANE + slot * 16);
-    hmeta[i] = (ok ? 1u : 0u) | ((in ? 1u : 0u) << 1) | (static_cast<uint32_t>(hr) << 8);
+    hoff[i] = static_cast<uint32_t>(((hr * W + wc) * g.C + hc * 8) * 2);
+    ok_s |= (ok ? 1u : 0u) << i;
+    top_m |= (in && hr == 0 ? 1u : 0u) << i;
+    bot_m |= (in && hr == TR + 1 ? 1u : 0u) << i;
+    in_m |= (in ? 1u : 0u) << i;
+  }
+  // a unit resource's range: through the last pixel of halo row TR + 1 ((TR + 2) W pixels past slot 0's)
+  const uint32_t hbytes = static_cast<uint32_t>(((TR + 2) * W + 1) * g.C * 2);
+  // ---- PRO == 0 with two halo buffers: no transform, so the halo goes global -> LDS by the buffer LDS-DMA
+  // without registers.  Wave w fills plane w (channels 8w .. 8w + 7 of the unit) in NBK blocks of 64
+  // consecutive slots (1 KiB each; the last block overlaps its predecessor -- duplicate writes of the same
+  // data -- so no block crosses into the next plane)
+  constexpr bool HDMA = PRO == 0 && NB == 2;
+  constexpr int NSL = S::PLANE / 16, NBK = (NSL + 63) / 64;
+  static_assert(NSL >= 64, "halo DMA blocks");
+  auto blk0 = [](int b) __attribute__((always_inline)) { return 64 * b < NSL - 64 ? 64 * b : NSL - 64; };
+  uint32_t dof[NBK];
+  uint32_t dok = 0, dtop = 0, dbot = 0;  // bit b: as ok_s / top_m / bot_m for the lane's slot of block b
+  if (HDMA) {
+#pragma unroll
+    for (int b = 0; b < NBK; ++b) {
+      const int slot = blk0(b) + lane;
+      const int hr = slot / S::RS, wc = slot - (slot / S::RS) * S::RS;
+      const bool in = slot < S::HS;
+      dof[b] = static_cast<uint32_t>(((hr * W + wc) * g.C + wave * 8) * 2);
+      dok |= (in && wc >= 1 && wc <= W ? 1u : 0u) << b;
+      dtop |= (in && hr == 0 ? 1u : 0u) << b;
+      dbot |= (in && hr == TR + 1 ? 1u : 0u) << b;
+    }
   }
   // ---- B-fragment bases: lane pixel p = wp0 + 16 j + rho = (image row p / WR, column p % WR) -> slot of
   // tap (0, 0) = row * RS + column; chunk lg of k-half 0 (k-half 1: + 4 planes, an immediate)
@@ -190,10 +236,10 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
     const int p = wp0 + 16 * j + rho;
     const int s0 = p < S::P ? (p / S::WR) * S::RS + (p - (p / S::WR) * S::WR) : 0;
     bb[0][j] = static_cast<uint32_t>(s0 * 16 + lg * S::PLANE);
-    bb[1][j] = bb[0][j] + S::HB;
+    bb[1][j] = bb[0][j] + (NB == 2 ? S::HB : 0);
   }
   // ---- A-fragment (weight) offsets in ring slot 0 (+ slot * WSLOT per item)
-  const uint32_t wts_b = 2u * S::HB;
+  const uint32_t wts_b = static_cast<uint32_t>(NB * S::HB);
   uint32_t aoff[2][FI];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
@@ -232,22 +278,42 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   };
   static_assert(8 + RING - 1 + RING - 1 < 4 * RING, "ring(): slot + tap lookahead range");
 
-  // ---- register-staged halo of one unit (native vectors: an aggregate select would go to scratch)
+  // ---- register-staged halo of one unit (native vectors: an aggregate select would go to scratch): loaded
+  // at tap 0, stored at tap HST
+  constexpr int HST = 5;
   u32x4 hx[NCH], hy[PRO == 2 ? NCH : 1];
   int h_tile = 0, h_cb = 0;
+  uint32_t h_ok = 0;  // bit i: chunk i of the staged unit holds image data
   auto load_halo = [&](int u) __attribute__((always_inline)) {
     h_tile = unit_tile(u);
     h_cb = unit_cb(u);
     const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
-    const int64_t base = (static_cast<int64_t>(n) * g.H + h0) * W * g.C + h_cb * kBK;
+    h_ok = ok_s & (h0 == 0 ? ~top_m : ~0u) & (h0 + TR == g.H ? ~bot_m : ~0u);
+    const int64_t base = ((static_cast<int64_t>(n) * g.H + h0) * W - (W + 1)) * g.C + h_cb * kBK;
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x + base), 0, static_cast<int>(hbytes), 0x00020000);
+    __amdgpu_buffer_rsrc_t rr = rx;
+    if (PRO == 2)
+      rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(pa.res + base), 0, static_cast<int>(hbytes),
+                                             0x00020000);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int hr = static_cast<int>(hmeta[i] >> 8);
-      const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
-      const int64_t off = ok ? base + hrel[i] : 0;  // clamped: zeroed at the store
-      hx[i] = *reinterpret_cast<const u32x4*>(x + off);
-      if (PRO == 2) hy[i] = *reinterpret_cast<const u32x4*>(pa.res + off);
+      const uint32_t off = (h_ok >> i) & 1u ? hoff[i] : 0x80000000u;
+      hx[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+      if (PRO == 2) hy[i] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
     }
+  };
+  auto dma_halo = [&](int u, int buf) __attribute__((always_inline)) {  // HDMA
+    const int tile = unit_tile(u), cb = unit_cb(u);
+    const int n = tile / tiles_per_img, h0 = (tile - n * tiles_per_img) * TR;
+    const uint32_t okm = dok & (h0 == 0 ? ~dtop : ~0u) & (h0 + TR == g.H ? ~dbot : ~0u);
+    const int64_t base = ((static_cast<int64_t>(n) * g.H + h0) * W - (W + 1)) * g.C + cb * kBK;
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x + base), 0, static_cast<int>(hbytes), 0x00020000);
+    char* dst = halo + buf * S::HB + wave * S::PLANE;
+#pragma unroll
+    for (int b = 0; b < NBK; ++b)
+      dma16b(rx, (okm >> b) & 1u ? dof[b] : 0x80000000u, 0, dst + blk0(b) * 16);
   };
   auto store_halo = [&](int buf) __attribute__((always_inline)) {
     const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
@@ -256,17 +322,17 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       const int c0 = h_cb * kBK + hc * 8;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        fs[e] = pa.scale[c0 + e];
-        fh[e] = pa.shift[c0 + e];
-        fr[e] = PRO == 2 ? pa.rscale[c0 + e] : 0.f;
+        fs[e] = ppar[c0 + e];
+        fh[e] = ppar[g.C + c0 + e];
+        fr[e] = PRO == 2 ? ppar[2 * g.C + c0 + e] : 0.f;
       }
     }
-    const int64_t tile_pix0 = (static_cast<int64_t>(n) * g.H + h0) * W;
+    // slot 0's pixel, channel block h_cb (elements)
+    const int64_t slot0 = ((static_cast<int64_t>(n) * g.H + h0) * W - (W + 1)) * g.C + h_cb * kBK;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      if (!(hmeta[i] & 2u)) continue;  // beyond the halo (last round of chunks)
-      const int hr = static_cast<int>(hmeta[i] >> 8);
-      const bool ok = (hmeta[i] & 1u) && h0 - 1 + hr >= 0 && h0 - 1 + hr < g.H;
+      if (!((in_m >> i) & 1u)) continue;  // beyond the halo (last round of chunks)
+      const bool ok = (h_ok >> i) & 1u;
       u32x4 o;
       if (PRO) {
         float v[8];
@@ -283,13 +349,12 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
           o[e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
         }
       } else {
-        const uint32_t keep = ok ? 0xffffffffu : 0u;
-        o = hx[i] & keep;
+        o = hx[i];  // zeros outside the image (out-of-range buffer loads)
       }
-      *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds[i]) = o;
+      *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds0 + 2 * NT * i) = o;
       // the tile's own rows: the transformed operand is an output (weight gradient / BN backward)
-      if (PRO && pa.aout != nullptr && ct == 0 && ok && hr >= 1 && hr <= TR)
-        *reinterpret_cast<u32x4*>(pa.aout + tile_pix0 * g.C + hrel[i] + h_cb * kBK) = o;
+      if (PRO && pa.aout != nullptr && ct == 0 && ok && !((top_m >> i) & 1u) && !((bot_m >> i) & 1u))
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(pa.aout + slot0) + hoff[i]) = o;
     }
   };
 
@@ -376,28 +441,32 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   const char* lds_c = lds;
   auto ld = [&](uint32_t off) __attribute__((always_inline)) { return *reinterpret_cast<const s8*>(lds_c + off); };
 
-  // fragment double buffer: set P holds the operands of the item being multiplied, set P ^ 1 is being
-  // prefetched for the next item (P = item parity, compile-time inside the 18-tap unroll)
-  s8 fa[2][2][FI], fb[2][2][FJ];
-  // load the fragments of an item (tap T, halo buffer B: compile-time; its weights in ring slot `slot`) into
-  // set SET
-  auto fetch = [&](auto TT, auto BUF, auto SET, int slot) __attribute__((always_inline)) {
-    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value, SE = decltype(SET)::value;
+  // one register set of fragments, read after the tap's barrier (the other wave on the SIMD multiplies
+  // meanwhile)
+  s8 fa[2][FI], fb[2][FJ];
+  // load the fragments of an item (tap T, halo buffer B: compile-time; its weights in ring slot `slot`)
+  auto fetch = [&](auto TT, auto BUF, int slot) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value;
     constexpr uint32_t toff = static_cast<uint32_t>(((T / 3) * S::RS + (T % 3)) * 16);
     const uint32_t roff = static_cast<uint32_t>(slot * S::WSLOT);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < FI; ++i) fa[SE][kk][i] = ld(aoff[kk][i] + roff);
+      for (int i = 0; i < FI; ++i) fa[kk][i] = ld(aoff[kk][i] + roff);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) fb[SE][kk][j] = ld(bb[B][j] + toff + kk * 4 * S::PLANE);
+      for (int j = 0; j < FJ; ++j) fb[kk][j] = ld(bb[B][j] + toff + kk * 4 * S::PLANE);
     }
   };
 
-  // ---- prologue: unit 0's halo into buffer 0, weight items 0 .. 3 in flight, item 0's fragments
+  // ---- prologue: unit 0's halo into buffer 0, weight items 0 .. 3 in flight
   if (units > 0) {
-    load_halo(0);
-    store_halo(0);
+    if constexpr (HDMA) {
+      dma_halo(0, 0);
+    } else {
+      load_halo(0);
+      if (PRO) __syncthreads();  // ppar
+      store_halo(0);
+    }
     const int cb0 = unit_cb(0), cb1 = units > 1 ? unit_cb(1) : 0;
 #pragma unroll
     for (int it = 0; it < RING - 1; ++it)
@@ -406,61 +475,72 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    fetch(IC<0>{}, IC<0>{}, IC<0>{}, 0);
   }
 
-  // one tap: item it = u * 9 + T; operands in set SE (loaded during the previous tap).  rs0: ring slot of
-  // item u * 9; wo_u / wo_n: channel-block byte offsets of units u and u + 1 in a weight row
-  auto tap = [&](auto TT, auto BUF, auto SET, int u, int it, int rs0, int wo_u, int wo_n)
-      __attribute__((always_inline)) {
-    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value, SE = decltype(SET)::value;
-    // item it+1's weights landed (own DMA; the barrier makes every wave's visible).  Younger VMEM ops:
-    // the DMAs of items it+2, it+3 and, at T = 1..3, the next unit's halo loads issued at T = 0
-    const bool hl = (T >= 1 && T <= 3) && u + 1 < units;
+  // one tap: item it = u * 9 + T.  rs0: ring slot of item u * 9; wo_u / wo_n: channel-block byte offsets of
+  // units u and u + 1 in a weight row
+  auto tap = [&](auto TT, auto BUF, int u, int it, int rs0, int wo_u, int wo_n) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value, B = decltype(BUF)::value;
+    // item it's weights landed (own DMA; the barrier makes every wave's visible).  Younger VMEM ops: the
+    // DMAs of items it+1 .. it+3 and, at taps 1 .. 4, the next unit's halo loads issued at tap 0 after the
+    // DMA of item it (VMEM loads complete in issue order)
+    constexpr int YH = (T >= 1 && T <= 4) ? (HDMA ? NBK : NCH * LPC) : 0;
+    const bool hl = YH > 0 && u + 1 < units;
     if (it + 3 < nitems) {
-      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW + NCH * LPC) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW) : "memory");
+      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * NIW + YH) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * NIW) : "memory");
     } else if (it + 2 < nitems) {
-      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW + NCH * LPC) : "memory");
+      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW + YH) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIW) : "memory");
+    } else if (it + 1 < nitems) {
+      if (hl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW + YH) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIW) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own halo stores and this item's fragments
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own halo stores and the last item's fragments
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + RING - 1 < nitems) {  // item it+4: its slot last held item it-1 (read before the barrier)
       constexpr int TN = T + RING - 1;
       issue_w(TN < 9 ? TN * 2 * g.C + wo_u : (TN - 9) * 2 * g.C + wo_n, ring(rs0, TN));
     }
-    if (T == 0 && u + 1 < units) load_halo(u + 1);
-    if (T == 4 && u + 1 < units) store_halo(B ^ 1);  // buffer B^1 was last read by unit u-1
-    // prefetch the next item's operands (tap T+1, or tap 0 of unit u+1 in the other halo buffer)
-    if (it + 1 < nitems) {
-      if constexpr (T < 8) fetch(IC<T + 1>{}, IC<B>{}, IC<SE ^ 1>{}, ring(rs0, T + 1));
-      else fetch(IC<0>{}, IC<B ^ 1>{}, IC<SE ^ 1>{}, ring(rs0, T + 1));
+    if (NB == 1 && T == 0 && u > 0) {  // this unit's halo (staged during unit u-1), once every wave is past
+      store_halo(0);                     // unit u-1's last fragment reads (the barrier above)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
+    if (u + 1 < units) {  // NB == 2: halo buffer B^1 was last read by unit u-1
+      if constexpr (HDMA) {
+        if (T == 0) dma_halo(u + 1, B ^ 1);
+      } else {
+        if (T == 0) load_halo(u + 1);
+        if (NB == 2 && T == HST) store_halo(B ^ 1);
+      }
+    }
+    fetch(TT, BUF, ring(rs0, T));
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[SE][kk][i], fb[SE][kk][j], acc[i][j]);
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[kk][i], fb[kk][j], acc[i][j]);
   };
   auto unit_body = [&](auto BUF, int u) __attribute__((always_inline)) {
-    constexpr int B = decltype(BUF)::value;  // = u & 1 = parity of the unit's first item (9u even iff u even)
+    // BUF = u & 1: the unit's halo buffer
     const int it = u * 9;
     const int rs0 = it % RING;
     const int wo_u = unit_cb(u) * kBK * 2, wo_n = u + 1 < units ? unit_cb(u + 1) * kBK * 2 : 0;
-    tap(IC<0>{}, BUF, IC<B>{}, u, it, rs0, wo_u, wo_n);
-    tap(IC<1>{}, BUF, IC<B ^ 1>{}, u, it + 1, rs0, wo_u, wo_n);
-    tap(IC<2>{}, BUF, IC<B>{}, u, it + 2, rs0, wo_u, wo_n);
-    tap(IC<3>{}, BUF, IC<B ^ 1>{}, u, it + 3, rs0, wo_u, wo_n);
-    tap(IC<4>{}, BUF, IC<B>{}, u, it + 4, rs0, wo_u, wo_n);
-    tap(IC<5>{}, BUF, IC<B ^ 1>{}, u, it + 5, rs0, wo_u, wo_n);
-    tap(IC<6>{}, BUF, IC<B>{}, u, it + 6, rs0, wo_u, wo_n);
-    tap(IC<7>{}, BUF, IC<B ^ 1>{}, u, it + 7, rs0, wo_u, wo_n);
-    tap(IC<8>{}, BUF, IC<B>{}, u, it + 8, rs0, wo_u, wo_n);
+    tap(IC<0>{}, BUF, u, it, rs0, wo_u, wo_n);
+    tap(IC<1>{}, BUF, u, it + 1, rs0, wo_u, wo_n);
+    tap(IC<2>{}, BUF, u, it + 2, rs0, wo_u, wo_n);
+    tap(IC<3>{}, BUF, u, it + 3, rs0, wo_u, wo_n);
+    tap(IC<4>{}, BUF, u, it + 4, rs0, wo_u, wo_n);
+    tap(IC<5>{}, BUF, u, it + 5, rs0, wo_u, wo_n);
+    tap(IC<6>{}, BUF, u, it + 6, rs0, wo_u, wo_n);
+    tap(IC<7>{}, BUF, u, it + 7, rs0, wo_u, wo_n);
+    tap(IC<8>{}, BUF, u, it + 8, rs0, wo_u, wo_n);
     if (unit_cb(u) == g.cblk - 1) epilogue(unit_tile(u));
   };
   for (int u = 0; u < units; u += 2) {
@@ -505,24 +585,29 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 
 // ------------------------------------------------------------------------------------------ host
 struct V2Cfg {
-  int W, TR, bco, wco, nw;
+  int W, TR, bco, wco, nb;
 };
-// 4 waves, each a 64-channel x 64-pixel tile (16 MFMAs per 4 + 4 fragment reads):
-// 0: 56x56 layers, 4-row tiles (64 co); 1: 28x28 layers, 4-row tiles (128 co, 2 co-waves);
-// 2: 14x14 layers, one image per tile (64 co)
-constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 4}, {28, 4, 128, 2, 4}, {14, 14, 64, 1, 4}};
+// 8 waves each.  0: 56x56 layers, 4-row tiles (64 co, 64x32 wave tiles); 1: 28x28 layers, 4-row tiles (128 co,
+// 2 co-waves, 64x32); 2 / 3: 14x14 layers, one image per tile (64 co / 128 co with 2 co-waves, 64x64 tiles);
+// 4: 56x56, 8-row tiles with 64x64 wave tiles (2/3 of the LDS reads per MFMA; the 10-row halo fits once:
+// written between units); 5: 28x28, 7-row tiles, 128 co, 64x64 wave tiles (1/8 of the lanes idle)
+constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 2}, {28, 4, 128, 2, 2}, {14, 14, 64, 1, 2},
+                         {14, 14, 128, 2, 2}, {56, 8, 64, 1, 1}, {28, 7, 128, 2, 2}};
 constexpr int kNumV2 = sizeof(kV2) / sizeof(kV2[0]);
 
-template <int W, int TR, int BCO, int WCO, int NW>
+template <int W, int TR, int BCO, int WCO, int NB>
 int lds_bytes() {
-  return Shape<W, TR, BCO, WCO, NW>::LDS;
+  return Shape<W, TR, BCO, WCO, NB>::LDS;
 }
 
-int v2_lds(int cfg) {
+int v2_lds(int cfg) {  // without the PRO coefficients
   switch (cfg) {
-    case 0: return lds_bytes<56, 4, 64, 1, 4>();
-    case 1: return lds_bytes<28, 4, 128, 2, 4>();
-    default: return lds_bytes<14, 14, 64, 1, 4>();
+    case 0: return lds_bytes<56, 4, 64, 1, 2>();
+    case 1: return lds_bytes<28, 4, 128, 2, 2>();
+    case 2: return lds_bytes<14, 14, 64, 1, 2>();
+    case 3: return lds_bytes<14, 14, 128, 2, 2>();
+    case 4: return lds_bytes<56, 8, 64, 1, 1>();
+    default: return lds_bytes<28, 7, 128, 2, 2>();
   }
 }
 
@@ -541,7 +626,7 @@ int damd_v2_supported(int C, int K, int R, int S, int stride, int pad, int H, in
   if (cfg < 0 || cfg >= kNumV2) return 0;
   const V2Cfg c = kV2[cfg];
   return R == 3 && S == 3 && stride == 1 && pad == 1 && W == c.W && H > 0 && H % c.TR == 0 && C % kBK == 0 &&
-         C > 0 && K % c.bco == 0 && v2_lds(cfg) <= 160 * 1024;
+         C > 0 && K % c.bco == 0 && v2_lds(cfg) + 12 * C <= 160 * 1024;
 }
 
 // stats-partial rows (= blocks per co tile) of a launch
@@ -589,28 +674,31 @@ int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, in
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
-  const int lds = v2_lds(cfg);
-#define V2L(W_, TR_, BCO_, WCO_, NW_, E_, P_)                                                                 \
+  const int lds = v2_lds(cfg) + (pro == 0 ? 0 : pro == 1 ? 8 * C : 12 * C);
+#define V2L(W_, TR_, BCO_, WCO_, NB_, E_, P_)                                                                 \
   do {                                                                                                       \
-    auto* kfn = conv3x3v2_kernel<W_, TR_, BCO_, WCO_, NW_, E_, P_>;                                           \
+    auto* kfn = conv3x3v2_kernel<W_, TR_, BCO_, WCO_, NB_, E_, P_>;                                           \
     DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-    DAMD_LAUNCH(kfn, grid, dim3(64 * NW_), lds, st, xp, wp, yp, part, g, ea, pa);                              \
+    DAMD_LAUNCH(kfn, grid, dim3(512), lds, st, xp, wp, yp, part, g, ea, pa);                              \
   } while (0)
-#define V2E(W_, TR_, BCO_, WCO_, NW_)                                                                         \
+#define V2E(W_, TR_, BCO_, WCO_, NB_)                                                                         \
   do {                                                                                                       \
-    if (epi == 0 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiNone, 0);                                     \
-    else if (epi == 1 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiStats, 0);                               \
-    else if (epi == 1 && pro == 1) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiStats, 1);                               \
-    else if (epi == 2 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbM, 0);                                \
-    else if (epi == 3 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbR, 0);                                \
-    else if (epi == 2 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbM, 2);                                \
-    else if (epi == 3 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NW_, kEpiBnbR, 2);                                \
+    if (epi == 0 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiNone, 0);                                     \
+    else if (epi == 1 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiStats, 0);                               \
+    else if (epi == 1 && pro == 1) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiStats, 1);                               \
+    else if (epi == 2 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbM, 0);                                \
+    else if (epi == 3 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbR, 0);                                \
+    else if (epi == 2 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbM, 2);                                \
+    else if (epi == 3 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbR, 2);                                \
     else return -4;                                                                                          \
   } while (0)
   switch (cfg) {
-    case 0: V2E(56, 4, 64, 1, 4); break;
-    case 1: V2E(28, 4, 128, 2, 4); break;
-    default: V2E(14, 14, 64, 1, 4); break;
+    case 0: V2E(56, 4, 64, 1, 2); break;
+    case 1: V2E(28, 4, 128, 2, 2); break;
+    case 2: V2E(14, 14, 64, 1, 2); break;
+    case 3: V2E(14, 14, 128, 2, 2); break;
+    case 4: V2E(56, 8, 64, 1, 1); break;
+    default: V2E(28, 7, 128, 2, 2); break;
   }
 #undef V2E
 #undef V2L

@@ -3,6 +3,7 @@
 # throughput fused vs stock and its kernel profile.
 source "$(dirname "$0")/gpu_lib.sh"
 step bench 420 python bench.py --steps 20 --warmup 5
+step bench256 300 python bench.py --batch 256 --steps 30 --warmup 8
 step prof_resnet 600 bash scripts/gpu_prof_resnet.sh 2048
 step bert_bench 300 python -u scripts/bert_bench.py --batch 64 --seq 128 --steps 30 --warmup 10
 rm -rf gpurun_out/prof_bert

@@ -42,7 +42,7 @@ def main():
     from determined_amd import ops
 
     e = ops.ext()
-    nv2 = 3
+    nv2 = e.conv_v2_num_cfgs()
     base = e.conv_num_cfgs() - nv2
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     out = open(a.out, "w")

@@ -23,7 +23,7 @@ def ext():
 def _v2_cfgs(ext, x, w):
     from determined_amd.ops import conv as C  # noqa: F401  (same cfg numbering as the tuner's)
 
-    base = ext.conv_num_cfgs() - 3
+    base = ext.conv_num_cfgs() - ext.conv_v2_num_cfgs()
     return [c for c in range(base, ext.conv_num_cfgs()) if ext.conv_supported(x, w, c, 1, 1)]
 
 
@@ -31,10 +31,11 @@ def _rand(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16).contiguous(memory_format=CL)
 
 
-# (n, cin, cout, H, W): one v2 config each plus multi channel-block (cin / 64 = 2, 3, 4: the weight ring
+# (n, cin, cout, H, W): one v2 config each plus multi channel-block (64-channel blocks 2, 4, 8: the weight ring
 # wraps at different taps per unit) / co-tile and non-square cases
 SHAPES = [(2, 64, 64, 56, 56), (1, 128, 128, 8, 56), (3, 128, 128, 28, 28), (2, 64, 256, 12, 28),
-          (3, 128, 128, 14, 14), (2, 256, 256, 14, 14), (1, 256, 64, 4, 56), (2, 192, 128, 8, 28)]
+          (3, 128, 128, 14, 14), (2, 256, 256, 14, 14), (1, 256, 64, 4, 56), (2, 128, 512, 8, 28),
+          (1, 256, 64, 8, 56), (2, 256, 128, 14, 28)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -137,7 +138,7 @@ def test_v2_dgrad_deferred_bn_apply(ext, shape):
 def test_v2_refuses_unsupported_geometry(ext):
     """W not one of the compiled widths, H not a multiple of the tile rows, stride 2: no v2 config."""
     w = _rand(64, 64, 3, 3)
-    base = ext.conv_num_cfgs() - 3
+    base = ext.conv_num_cfgs() - ext.conv_v2_num_cfgs()
     for shape in [(1, 64, 56, 30), (1, 64, 10, 56), (1, 64, 28, 27)]:
         x = _rand(*shape)
         assert not any(ext.conv_supported(x, w, c, 1, 1) for c in range(base, ext.conv_num_cfgs()))
