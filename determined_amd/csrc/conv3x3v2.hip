@@ -43,6 +43,7 @@ namespace c3v2 {
 typedef short s8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kBK = 64;      // channels per unit (one k-step of 64 per tap)
@@ -108,7 +109,7 @@ struct ProArgs {
 // pixel lanes are row-padded to WR = W rounded up to 16), and the ds_read_b128 lane groups
 // ({0-3, 12-15 | 20-27}, ...) mix two chunks of 8 + 8 slots: with PLANE a multiple of 256 bytes the 16
 // addresses of a group always fall in 16 distinct bank quads -- no swizzle, no conflict.
-template <int W, int TR, int BCO, int WCO, int NB>
+template <int W, int TR, int BCO, int WCO, int NB, int RES>
 struct Shape {
   static constexpr int NW = 8;
   static constexpr int RS = W + 2;                        // slots per halo row (zero column at both ends)
@@ -126,18 +127,21 @@ struct Shape {
   static constexpr int NCH = (HS * 8 + NT - 1) / NT;      // halo 16-byte chunks per thread
   static constexpr int NIW = BCO / (8 * NW);              // weight DMA instructions per wave per tap
   static constexpr int WSLOT = BCO * kBK * 2;             // bytes per weight ring slot
-  static constexpr int RING = 5;                          // weight ring slots (DMA 4 taps ahead)
+  // weight ring slots: 5 (DMA 4 taps ahead); RES: 9, one per tap, the 64-channel layer's whole filter
+  // resident in LDS for the launch (C == 64: every unit has the same weights)
+  static constexpr int RING = RES ? 9 : 5;
   static constexpr int LDS = NB * HB + RING * WSLOT + 3 * BCO * 4;  // + the PRO coefficients [2 or 3][C] fp32
   static_assert(FI % 2 == 0 && FJ >= 1 && BCO % (8 * NW) == 0 && WCO * PW == NW && (NB == 1 || NB == 2), "bad tile");
   static_assert(NT % 128 == 0 && NCH <= 16, "halo staging map");
   static_assert(4 * PLANE + ((2 * RS + 2) * 16) < 65536, "ds_read immediate offsets");
 };
 
-template <int W, int TR, int BCO, int WCO, int NB, int EPI, int PRO>
+template <int W, int TR, int BCO, int WCO, int NB, int RES, int EPI, int PRO>
 __global__ void __launch_bounds__(512, 1)
 conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
                  float* __restrict__ part, Geo g, EpiArgs ea, ProArgs pa) {
-  using S = Shape<W, TR, BCO, WCO, NB>;
+  using S = Shape<W, TR, BCO, WCO, NB, RES>;
+  static_assert(!RES || NB == 1, "resident weights: one halo buffer");
   constexpr int NW = S::NW;
   constexpr int FI = S::FI, FJ = S::FJ, NT = S::NT, NCH = S::NCH, NIW = S::NIW, RING = S::RING;
   constexpr bool SUMS = EPI != kEpiNone;
@@ -278,17 +282,24 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   };
   static_assert(8 + RING - 1 + RING - 1 < 4 * RING, "ring(): slot + tap lookahead range");
 
-  // ---- register-staged halo of one unit (native vectors: an aggregate select would go to scratch): loaded
-  // at tap 0, stored at tap HST
-  constexpr int HST = 5;
+  // ---- register-staged halo of one unit (native vectors: an aggregate select would go to scratch).  Three
+  // steps: load (global -> registers), transform (PRO: BN affine / ReLU / residual, zero outside the image,
+  // packed to bf16 in place) and write (registers -> LDS, plus the transformed operand to pa.aout).  NB == 2:
+  // loaded at tap 0, transformed and written at tap HST.  RES: loaded and transformed in two halves during
+  // the unit's taps, written at the next unit boundary (between two barriers, so only the LDS stores remain
+  // there)
+  constexpr int HST = 5, NH = (NCH + 1) / 2;
   u32x4 hx[NCH], hy[PRO == 2 ? NCH : 1];
   int h_tile = 0, h_cb = 0;
   uint32_t h_ok = 0;  // bit i: chunk i of the staged unit holds image data
-  auto load_halo = [&](int u) __attribute__((always_inline)) {
-    h_tile = unit_tile(u);
-    h_cb = unit_cb(u);
+  auto load_halo = [&](int u, auto I0, auto I1) __attribute__((always_inline)) {
+    constexpr int A = decltype(I0)::value, Z = decltype(I1)::value;
+    if (A == 0) {
+      h_tile = unit_tile(u);
+      h_cb = unit_cb(u);
+    }
     const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
-    h_ok = ok_s & (h0 == 0 ? ~top_m : ~0u) & (h0 + TR == g.H ? ~bot_m : ~0u);
+    if (A == 0) h_ok = ok_s & (h0 == 0 ? ~top_m : ~0u) & (h0 + TR == g.H ? ~bot_m : ~0u);
     const int64_t base = ((static_cast<int64_t>(n) * g.H + h0) * W - (W + 1)) * g.C + h_cb * kBK;
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x + base), 0, static_cast<int>(hbytes), 0x00020000);
@@ -297,7 +308,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(pa.res + base), 0, static_cast<int>(hbytes),
                                              0x00020000);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
+    for (int i = A; i < Z; ++i) {
       const uint32_t off = (h_ok >> i) & 1u ? hoff[i] : 0x80000000u;
       hx[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
       if (PRO == 2) hy[i] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
@@ -315,47 +326,53 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
     for (int b = 0; b < NBK; ++b)
       dma16b(rx, (okm >> b) & 1u ? dof[b] : 0x80000000u, 0, dst + blk0(b) * 16);
   };
-  auto store_halo = [&](int buf) __attribute__((always_inline)) {
-    const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
+  auto xform_halo = [&](auto I0, auto I1) __attribute__((always_inline)) {  // PRO only
+    constexpr int A = decltype(I0)::value, Z = decltype(I1)::value;
+    if (!PRO) return;
     float fs[8], fh[8], fr[8];
-    if (PRO) {
-      const int c0 = h_cb * kBK + hc * 8;
+    const int c0 = h_cb * kBK + hc * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fs[e] = ppar[c0 + e];
+      fh[e] = ppar[g.C + c0 + e];
+      fr[e] = PRO == 2 ? ppar[2 * g.C + c0 + e] : 0.f;
+    }
+#pragma unroll
+    for (int i = A; i < Z; ++i) {
+      const bool ok = (h_ok >> i) & 1u;
+      float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        fs[e] = ppar[c0 + e];
-        fh[e] = ppar[g.C + c0 + e];
-        fr[e] = PRO == 2 ? ppar[2 * g.C + c0 + e] : 0.f;
+        const float xv = bf_lo(hx[i][e >> 1], e & 1);
+        const float t = PRO == 2 ? fs[e] * xv + fr[e] * bf_lo(hy[i][e >> 1], e & 1) + fh[e]
+                                 : fmaxf(xv * fs[e] + fh[e], 0.f);
+        v[e] = ok ? t : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const u16v2_t pk = f2bf2(v[e], v[e + 1]);
+        hx[i][e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
       }
     }
+  };
+  auto write_halo = [&](int buf) __attribute__((always_inline)) {
+    const int n = h_tile / tiles_per_img, h0 = (h_tile - n * tiles_per_img) * TR;
     // slot 0's pixel, channel block h_cb (elements)
     const int64_t slot0 = ((static_cast<int64_t>(n) * g.H + h0) * W - (W + 1)) * g.C + h_cb * kBK;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       if (!((in_m >> i) & 1u)) continue;  // beyond the halo (last round of chunks)
-      const bool ok = (h_ok >> i) & 1u;
-      u32x4 o;
-      if (PRO) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xv = bf_lo(hx[i][e >> 1], e & 1);
-          const float t = PRO == 2 ? fs[e] * xv + fr[e] * bf_lo(hy[i][e >> 1], e & 1) + fh[e]
-                                   : fmaxf(xv * fs[e] + fh[e], 0.f);
-          v[e] = ok ? t : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const u16v2_t pk = f2bf2(v[e], v[e + 1]);
-          o[e >> 1] = static_cast<uint32_t>(pk[0]) | (static_cast<uint32_t>(pk[1]) << 16);
-        }
-      } else {
-        o = hx[i];  // zeros outside the image (out-of-range buffer loads)
-      }
-      *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds0 + 2 * NT * i) = o;
+      // PRO == 0: zeros outside the image come from the out-of-range buffer loads
+      *reinterpret_cast<u32x4*>(halo + buf * S::HB + hlds0 + 2 * NT * i) = hx[i];
       // the tile's own rows: the transformed operand is an output (weight gradient / BN backward)
-      if (PRO && pa.aout != nullptr && ct == 0 && ok && !((top_m >> i) & 1u) && !((bot_m >> i) & 1u))
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(pa.aout + slot0) + hoff[i]) = o;
+      if (PRO && pa.aout != nullptr && ct == 0 && ((h_ok >> i) & 1u) && !((top_m >> i) & 1u) &&
+          !((bot_m >> i) & 1u))
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(pa.aout + slot0) + hoff[i]) = hx[i];
     }
+  };
+  auto store_halo = [&](int buf) __attribute__((always_inline)) {
+    xform_halo(IC<0>{}, IC<NCH>{});
+    write_halo(buf);
   };
 
   f4 acc[FI][FJ];
@@ -363,11 +380,12 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float st_s[FI / 2][8], st_q[FI / 2][8];
+  // channel sums as pairs: the accumulation is packed fp32 math (v_pk_add_f32 / v_pk_fma_f32), half the VALU
+  f2 st_s[FI / 2][4], st_q[FI / 2][4];
 #pragma unroll
   for (int q = 0; q < FI / 2; ++q)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { st_s[q][e] = 0.f; st_q[q][e] = 0.f; }
+    for (int e = 0; e < 4; ++e) { st_s[q][e] = f2{0.f, 0.f}; st_q[q][e] = f2{0.f, 0.f}; }
 
   // ---- epilogue of one tile: lane (lg, rho) holds channels wco0 + 32q + 8lg + 0..7 of lane pixel p_j
   auto epilogue = [&](int tile) __attribute__((always_inline)) {
@@ -417,16 +435,18 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
           *reinterpret_cast<u32x4*>(y + m * g.K + static_cast<int64_t>(ct) * BCO + cl) = v;
           if (EPI == kEpiStats) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              st_s[q][e] += o[e];
-              st_q[q][e] += o[e] * o[e];
+            for (int e = 0; e < 4; ++e) {
+              const f2 ov = {o[2 * e], o[2 * e + 1]};
+              st_s[q][e] += ov;
+              st_q[q][e] = __builtin_elementwise_fma(ov, ov, st_q[q][e]);
             }
           } else if (EPI >= kEpiBnbM) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float f = bf_lo(v[e >> 1], e & 1);
-              st_s[q][e] += f;
-              st_q[q][e] += f * (yv[e] - prm[cl + e]);
+            for (int e = 0; e < 4; ++e) {
+              const f2 fv = {bf_lo(v[e], 0), bf_lo(v[e], 1)};
+              const f2 dv = f2{yv[2 * e], yv[2 * e + 1]} - f2{prm[cl + 2 * e], prm[cl + 2 * e + 1]};
+              st_s[q][e] += fv;
+              st_q[q][e] = __builtin_elementwise_fma(fv, dv, st_q[q][e]);
             }
           }
         }
@@ -458,18 +478,19 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
     }
   };
 
-  // ---- prologue: unit 0's halo into buffer 0, weight items 0 .. 3 in flight
+  // ---- prologue: unit 0's halo into buffer 0, weight items 0 .. 3 in flight (RES: all 9 taps)
+  constexpr int PRE = RES ? 9 : RING - 1;
   if (units > 0) {
     if constexpr (HDMA) {
       dma_halo(0, 0);
     } else {
-      load_halo(0);
+      load_halo(0, IC<0>{}, IC<NCH>{});
       if (PRO) __syncthreads();  // ppar
       store_halo(0);
     }
     const int cb0 = unit_cb(0), cb1 = units > 1 ? unit_cb(1) : 0;
 #pragma unroll
-    for (int it = 0; it < RING - 1; ++it)
+    for (int it = 0; it < PRE; ++it)
       if (it < nitems) issue_w(((it < 9 ? it : it - 9) * g.C + (it < 9 ? cb0 : cb1) * kBK) * 2, it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -515,7 +536,7 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       if constexpr (HDMA) {
         if (T == 0) dma_halo(u + 1, B ^ 1);
       } else {
-        if (T == 0) load_halo(u + 1);
+        if (T == 0) load_halo(u + 1, IC<0>{}, IC<NCH>{});
         if (NB == 2 && T == HST) store_halo(B ^ 1);
       }
     }
@@ -527,7 +548,50 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 #pragma unroll
         for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[kk][i], fb[kk][j], acc[i][j]);
   };
+  // RES: no weight traffic after the prologue, so no per-tap wait or barrier -- the waves only meet at unit
+  // boundaries, where the single halo buffer is rewritten
+  auto tap_res = [&](auto TT, int u) __attribute__((always_inline)) {
+    constexpr int T = decltype(TT)::value;
+    if (T == 0 && u > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is past unit u-1's fragment reads
+      asm volatile("" ::: "memory");
+      write_halo(0);  // transformed during unit u-1
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (u + 1 < units) {
+      if (T == 0) load_halo(u + 1, IC<0>{}, IC<NH>{});
+      if (T == 3) {
+        xform_halo(IC<0>{}, IC<NH>{});
+        asm volatile("" ::: "memory");  // keep the second half's loads here (register pressure)
+        load_halo(u + 1, IC<NH>{}, IC<NCH>{});
+      }
+      if (T == 7) xform_halo(IC<NH>{}, IC<NCH>{});
+    }
+    fetch(TT, IC<0>{}, T);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = mfma(fa[kk][i], fb[kk][j], acc[i][j]);
+  };
   auto unit_body = [&](auto BUF, int u) __attribute__((always_inline)) {
+    if constexpr (RES) {
+      tap_res(IC<0>{}, u);
+      tap_res(IC<1>{}, u);
+      tap_res(IC<2>{}, u);
+      tap_res(IC<3>{}, u);
+      tap_res(IC<4>{}, u);
+      tap_res(IC<5>{}, u);
+      tap_res(IC<6>{}, u);
+      tap_res(IC<7>{}, u);
+      tap_res(IC<8>{}, u);
+      epilogue(unit_tile(u));
+      return;
+    }
     // BUF = u & 1: the unit's halo buffer
     const int it = u * 9;
     const int rs0 = it % RING;
@@ -555,8 +619,8 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
       for (int e = 0; e < 8; ++e)
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
-          st_s[q][e] += __shfl_xor(st_s[q][e], o, 64);
-          st_q[q][e] += __shfl_xor(st_q[q][e], o, 64);
+          st_s[q][e >> 1][e & 1] += __shfl_xor(st_s[q][e >> 1][e & 1], o, 64);
+          st_q[q][e >> 1][e & 1] += __shfl_xor(st_q[q][e >> 1][e & 1], o, 64);
         }
     __syncthreads();
     constexpr int WPW = S::PW;
@@ -568,8 +632,8 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int co = wco0 + 32 * q + 8 * lg + e;
-          red[(wpi * 2) * BCO + co] = st_s[q][e];
-          red[(wpi * 2 + 1) * BCO + co] = st_q[q][e];
+          red[(wpi * 2) * BCO + co] = st_s[q][e >> 1][e & 1];
+          red[(wpi * 2 + 1) * BCO + co] = st_q[q][e >> 1][e & 1];
         }
     }
     __syncthreads();
@@ -585,29 +649,31 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
 
 // ------------------------------------------------------------------------------------------ host
 struct V2Cfg {
-  int W, TR, bco, wco, nb;
+  int W, TR, bco, wco, nb, res;
 };
 // 8 waves each.  0: 56x56 layers, 4-row tiles (64 co, 64x32 wave tiles); 1: 28x28 layers, 4-row tiles (128 co,
 // 2 co-waves, 64x32); 2 / 3: 14x14 layers, one image per tile (64 co / 128 co with 2 co-waves, 64x64 tiles);
 // 4: 56x56, 8-row tiles with 64x64 wave tiles (2/3 of the LDS reads per MFMA; the 10-row halo fits once:
-// written between units); 5: 28x28, 7-row tiles, 128 co, 64x64 wave tiles (1/8 of the lanes idle)
-constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 2}, {28, 4, 128, 2, 2}, {14, 14, 64, 1, 2},
-                         {14, 14, 128, 2, 2}, {56, 8, 64, 1, 1}, {28, 7, 128, 2, 2}};
+// written between units); 5: 28x28, 7-row tiles, 128 co, 64x64 wave tiles (1/8 of the lanes idle); 6: as 4
+// with the 64-channel filter resident in LDS (C == 64), no per-tap barrier
+constexpr V2Cfg kV2[] = {{56, 4, 64, 1, 2, 0},  {28, 4, 128, 2, 2, 0}, {14, 14, 64, 1, 2, 0}, {14, 14, 128, 2, 2, 0},
+                         {56, 8, 64, 1, 1, 0}, {28, 7, 128, 2, 2, 0}, {56, 8, 64, 1, 1, 1}};
 constexpr int kNumV2 = sizeof(kV2) / sizeof(kV2[0]);
 
-template <int W, int TR, int BCO, int WCO, int NB>
+template <int W, int TR, int BCO, int WCO, int NB, int RES>
 int lds_bytes() {
-  return Shape<W, TR, BCO, WCO, NB>::LDS;
+  return Shape<W, TR, BCO, WCO, NB, RES>::LDS;
 }
 
 int v2_lds(int cfg) {  // without the PRO coefficients
   switch (cfg) {
-    case 0: return lds_bytes<56, 4, 64, 1, 2>();
-    case 1: return lds_bytes<28, 4, 128, 2, 2>();
-    case 2: return lds_bytes<14, 14, 64, 1, 2>();
-    case 3: return lds_bytes<14, 14, 128, 2, 2>();
-    case 4: return lds_bytes<56, 8, 64, 1, 1>();
-    default: return lds_bytes<28, 7, 128, 2, 2>();
+    case 0: return lds_bytes<56, 4, 64, 1, 2, 0>();
+    case 1: return lds_bytes<28, 4, 128, 2, 2, 0>();
+    case 2: return lds_bytes<14, 14, 64, 1, 2, 0>();
+    case 3: return lds_bytes<14, 14, 128, 2, 2, 0>();
+    case 4: return lds_bytes<56, 8, 64, 1, 1, 0>();
+    case 5: return lds_bytes<28, 7, 128, 2, 2, 0>();
+    default: return lds_bytes<56, 8, 64, 1, 1, 1>();
   }
 }
 
@@ -626,7 +692,7 @@ int damd_v2_supported(int C, int K, int R, int S, int stride, int pad, int H, in
   if (cfg < 0 || cfg >= kNumV2) return 0;
   const V2Cfg c = kV2[cfg];
   return R == 3 && S == 3 && stride == 1 && pad == 1 && W == c.W && H > 0 && H % c.TR == 0 && C % kBK == 0 &&
-         C > 0 && K % c.bco == 0 && v2_lds(cfg) + 12 * C <= 160 * 1024;
+         C > 0 && K % c.bco == 0 && (c.res == 0 || C == kBK) && v2_lds(cfg) + 12 * C <= 160 * 1024;
 }
 
 // stats-partial rows (= blocks per co tile) of a launch
@@ -675,30 +741,31 @@ int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, in
   const bf16_t* wp = static_cast<const bf16_t*>(w);
   bf16_t* yp = static_cast<bf16_t*>(y);
   const int lds = v2_lds(cfg) + (pro == 0 ? 0 : pro == 1 ? 8 * C : 12 * C);
-#define V2L(W_, TR_, BCO_, WCO_, NB_, E_, P_)                                                                 \
+#define V2L(W_, TR_, BCO_, WCO_, NB_, R_, E_, P_)                                                                 \
   do {                                                                                                       \
-    auto* kfn = conv3x3v2_kernel<W_, TR_, BCO_, WCO_, NB_, E_, P_>;                                           \
+    auto* kfn = conv3x3v2_kernel<W_, TR_, BCO_, WCO_, NB_, R_, E_, P_>;                                           \
     DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     DAMD_LAUNCH(kfn, grid, dim3(512), lds, st, xp, wp, yp, part, g, ea, pa);                              \
   } while (0)
-#define V2E(W_, TR_, BCO_, WCO_, NB_)                                                                         \
+#define V2E(W_, TR_, BCO_, WCO_, NB_, R_)                                                                         \
   do {                                                                                                       \
-    if (epi == 0 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiNone, 0);                                     \
-    else if (epi == 1 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiStats, 0);                               \
-    else if (epi == 1 && pro == 1) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiStats, 1);                               \
-    else if (epi == 2 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbM, 0);                                \
-    else if (epi == 3 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbR, 0);                                \
-    else if (epi == 2 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbM, 2);                                \
-    else if (epi == 3 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, kEpiBnbR, 2);                                \
+    if (epi == 0 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiNone, 0);                                     \
+    else if (epi == 1 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiStats, 0);                               \
+    else if (epi == 1 && pro == 1) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiStats, 1);                               \
+    else if (epi == 2 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiBnbM, 0);                                \
+    else if (epi == 3 && pro == 0) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiBnbR, 0);                                \
+    else if (epi == 2 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiBnbM, 2);                                \
+    else if (epi == 3 && pro == 2) V2L(W_, TR_, BCO_, WCO_, NB_, R_, kEpiBnbR, 2);                                \
     else return -4;                                                                                          \
   } while (0)
   switch (cfg) {
-    case 0: V2E(56, 4, 64, 1, 2); break;
-    case 1: V2E(28, 4, 128, 2, 2); break;
-    case 2: V2E(14, 14, 64, 1, 2); break;
-    case 3: V2E(14, 14, 128, 2, 2); break;
-    case 4: V2E(56, 8, 64, 1, 1); break;
-    default: V2E(28, 7, 128, 2, 2); break;
+    case 0: V2E(56, 4, 64, 1, 2, 0); break;
+    case 1: V2E(28, 4, 128, 2, 2, 0); break;
+    case 2: V2E(14, 14, 64, 1, 2, 0); break;
+    case 3: V2E(14, 14, 128, 2, 2, 0); break;
+    case 4: V2E(56, 8, 64, 1, 1, 0); break;
+    case 5: V2E(28, 7, 128, 2, 2, 0); break;
+    default: V2E(56, 8, 64, 1, 1, 1); break;
   }
 #undef V2E
 #undef V2L
