@@ -70,7 +70,8 @@ extern "C" int damd_conv1x1_bwd_fused_blocks(int64_t);
 extern "C" int damd_conv1x1_bwd_fused_launch(const void*, const void*, const float*, const void*, const void*,
                                              const void*, const float*, int64_t, void*, float*, float*, void*, int,
                                              int, int, hipStream_t);
-extern "C" int damd_wgrad3x3_supported(int, int, int, int);
+extern "C" int damd_wgrad3x3_supported(int, int, int, int, int);
+extern "C" int damd_wgrad3x3_num_cfgs();
 extern "C" int damd_wgrad3x3_splits(int64_t, int, int, int, int, int, int);
 extern "C" int damd_wgrad3x3_launch(const void*, const void*, float*, void*, int, int, int, int, int, int, int, int,
                                     hipStream_t);
@@ -1261,14 +1262,15 @@ at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tenso
 }
 
 // dW of a 3x3 / stride-1 / pad-1 convolution by the halo kernel (cfg 0: 128 output channels per
-// block, 1: 64), in w's dtype, channels-last [K, C, 3, 3].
+// block, 1: 64; 2 ..: conv3x3v2.hip's whole-row-tile kernel), in w's dtype, channels-last [K, C, 3, 3].
 bool wgrad3x3_supported(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& w, int64_t cfg) {
   return x.is_cuda() && x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
          dy.dim() == 4 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
          dy.size(1) == w.size(0) && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) && dy.size(3) == x.size(3) &&
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
          (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 &&
-         damd_wgrad3x3_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(x.size(3)),
+         damd_wgrad3x3_supported(static_cast<int>(x.size(1)), static_cast<int>(w.size(0)), static_cast<int>(x.size(2)),
+                                 static_cast<int>(x.size(3)),
                                  static_cast<int>(cfg));
 }
 
@@ -1552,6 +1554,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported);
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
+  m.def("wgrad3x3_num_cfgs", &damd_wgrad3x3_num_cfgs);
   m.def("conv_sk_timeouts", &conv_sk_timeouts, py::arg("like"), py::arg("reset") = false);
   m.def("conv_dgrad_phase", &conv_dgrad_phase);
   m.def("conv_sk_cfg", [](int64_t cfg) { return damd_conv_cfg_is_sk(static_cast<int>(cfg)) != 0; });

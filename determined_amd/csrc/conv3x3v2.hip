@@ -647,6 +647,173 @@ conv3x3v2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf1
   }
 }
 
+// ============================================================ 3x3 / stride-1 weight gradient
+// dW[co][r][s][ci] = sum_p dY[p][co] x[p + (r - 1, s - 1)][ci] on the same whole-row tiles: a stage is TR
+// image rows of one image -- the dY tile (64 output channels) and the input's zero-padded halo (64 input
+// channels) -- both LDS-DMA'd as 8-channel planes (out-of-range offsets give the zero border), and each
+// wave reduces the stage's pixels into all 9 taps of its (32 co x 16 ci) tile.  The MFMA's reduction
+// index is the pixel, so both operands are read with ds_read_b64_tr_b16 (4 pixels x 16 channels per
+// 16-lane group, delivered channel-major): a lane's address is (its pixel slot, its plane) -- a lane base
+// register per 16-pixel half-step and immediates for the tap, plane and step: no VALU per read.  Plane
+// pitches are 128 (mod 256) bytes, so the two planes a 32-lane half touches sit 32 banks apart.  Lane
+// pixels are row-padded to a multiple of 4 (a transposed read's 4 rows stay in one image row); pad pixels
+// carry zero dY.  Blocks = (64 co, 64 ci) tiles x pixel splits; every block writes its partial dW slab
+// and conv_igemm.hip's wgrad_finalize_kernel sums them (deterministic).
+// Reference counterpart: the cuDNN weight-gradient call in harness/determined/pytorch/_pytorch_trial.py's
+// training step (backward of torch.nn.Conv2d).
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
+
+constexpr int wpitch(int b) { return b <= 128 ? 128 : (b - 128 + 255) / 256 * 256 + 128; }
+
+template <int W, int TR, int WR_>
+struct WShape {
+  static constexpr int WR = WR_;               // lane pixels per image row (>= W, a multiple of 4)
+  static constexpr int P = TR * WR;            // lane pixels per stage
+  static constexpr int KS = P / 32;            // k-steps per stage
+  static constexpr int RS = W + 2, HS = (TR + 2) * RS;
+  static constexpr int XS = WR + 2 > RS ? WR + 2 - RS : 0;  // slots past HS that pad pixels' taps read
+  static constexpr int XPL = wpitch((HS + XS) * 16);        // x halo plane pitch (8 channels)
+  static constexpr int DPL = wpitch(P * 16);                // dY plane pitch
+  static constexpr int XB = 8 * XPL, SB = XB + 8 * DPL;     // x image / stage bytes
+  static constexpr int LDS = 2 * SB;
+  static constexpr int NXS = XPL / 16, NXB = (NXS + 63) / 64;  // x plane slots, 64-slot DMA blocks
+  static constexpr int NDB = (P + 63) / 64;                    // dY 64-pixel DMA blocks
+  static_assert(WR >= W && WR % 4 == 0 && P % 32 == 0 && P >= 64 && NXS >= 64 && NXB <= 32 && NDB <= 32,
+                "wgrad stage shape");
+};
+
+struct WGeo {
+  int N, H, C, K;
+  int cotiles, cblks, splits, stages;  // stages = N * H / TR
+};
+
+template <int W, int TR, int WR>
+__global__ void __launch_bounds__(512, 1)
+conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part,
+                       WGeo g) {
+  using S = WShape<W, TR, WR>;
+  constexpr int KS = S::KS;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wco = wave >> 2, cig = wave & 3;  // 32 output channels x 16 input channels per wave
+
+  const int nblk = gridDim.x, L = blockIdx.x;
+  const int xcd = L & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ntile = g.cotiles * g.cblks;
+  const int tile = rid % ntile, split = rid / ntile;
+  const int cot = tile % g.cotiles, cb = tile / g.cotiles;
+  const int s_begin = static_cast<int>(static_cast<int64_t>(split) * g.stages / g.splits);
+  const int s_end = static_cast<int>(static_cast<int64_t>(split + 1) * g.stages / g.splits);
+  const int items = s_end - s_begin;
+  const int tiles_per_img = g.H / TR;
+
+  // ---- DMA roles: wave w fills x plane w (input channels 8w .. 8w + 7 of the block) and dY plane w
+  // (output channels 8w .. 8w + 7) in 64-slot blocks; the last block of a plane overlaps its predecessor
+  auto bx0 = [](int b) __attribute__((always_inline)) { return 64 * b < S::NXS - 64 ? 64 * b : S::NXS - 64; };
+  auto bd0 = [](int b) __attribute__((always_inline)) { return 64 * b < S::P - 64 ? 64 * b : S::P - 64; };
+  uint32_t xof[S::NXB], dof[S::NDB];
+  uint32_t xok = 0, xtop = 0, xbot = 0, dok = 0;
+#pragma unroll
+  for (int b = 0; b < S::NXB; ++b) {
+    const int slot = bx0(b) + lane;
+    const int hr = slot / S::RS, wc = slot - (slot / S::RS) * S::RS;
+    const bool in = slot < S::HS;
+    xof[b] = static_cast<uint32_t>(((hr * W + wc) * g.C + wave * 8) * 2);
+    xok |= (in && wc >= 1 && wc <= W ? 1u : 0u) << b;
+    xtop |= (in && hr == 0 ? 1u : 0u) << b;
+    xbot |= (in && hr == TR + 1 ? 1u : 0u) << b;
+  }
+#pragma unroll
+  for (int b = 0; b < S::NDB; ++b) {
+    const int p = bd0(b) + lane;
+    const int row = p / S::WR, col = p - (p / S::WR) * S::WR;
+    dof[b] = static_cast<uint32_t>(((row * W + col) * g.K + wave * 8) * 2);
+    dok |= (col < W ? 1u : 0u) << b;
+  }
+  const uint32_t xbytes = static_cast<uint32_t>(((TR + 2) * W + 1) * g.C * 2);
+  const uint32_t dbytes = static_cast<uint32_t>(TR * W * g.K * 2);
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    const int n = st / tiles_per_img, h0 = (st - n * tiles_per_img) * TR;
+    const int64_t pix0 = (static_cast<int64_t>(n) * g.H + h0) * W;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(x + (pix0 - (W + 1)) * g.C + cb * 64), 0, static_cast<int>(xbytes), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(dy + pix0 * g.K + cot * 64), 0, static_cast<int>(dbytes), 0x00020000);
+    const uint32_t okm = xok & (h0 == 0 ? ~xtop : ~0u) & (h0 + TR == g.H ? ~xbot : ~0u);
+    char* xd = lds + buf * S::SB + wave * S::XPL;
+    char* dd = lds + buf * S::SB + S::XB + wave * S::DPL;
+#pragma unroll
+    for (int b = 0; b < S::NXB; ++b) dma16b(rx, (okm >> b) & 1u ? xof[b] : 0x80000000u, 0, xd + bx0(b) * 16);
+#pragma unroll
+    for (int b = 0; b < S::NDB; ++b) dma16b(rd, (dok >> b) & 1u ? dof[b] : 0x80000000u, 0, dd + bd0(b) * 16);
+  };
+
+  // ---- transposed-read lane bases: lane 4q + p of a 16-lane group addresses row (pixel) q, columns
+  // (channels) 4p .. 4p + 3 = plane p >> 1, byte 8 (p & 1) of the 16-byte slot; group lg takes pixels
+  // 4lg .. 4lg + 3 of each 16-pixel half-step
+  const int i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3, lg = lane >> 4;
+  const uint32_t a_l = static_cast<uint32_t>(S::XB + (4 * wco + (pp >> 1)) * S::DPL + 8 * (pp & 1) +
+                                             16 * (4 * lg + qq));
+  uint32_t b_l[KS][2];  // x slot of the lane's pixel for tap (0, 0), per half-step
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int px = 32 * ks + 16 * h + 4 * lg + qq;
+      const int row = px / S::WR, col = px - (px / S::WR) * S::WR;
+      b_l[ks][h] = static_cast<uint32_t>((2 * cig + (pp >> 1)) * S::XPL + 8 * (pp & 1) + 16 * (row * S::RS + col));
+    }
+  auto tr8 = [&](uint32_t lo, uint32_t hi) __attribute__((always_inline)) {
+    const s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + lo));
+    const s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + hi));
+    s8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
+  };
+
+  f4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (items > 0) issue(s_begin, 0);
+  for (int it = 0; it < items; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage it landed for every wave; stage it-1 is no longer read
+    if (it + 1 < items) issue(s_begin + it + 1, (it + 1) & 1);
+    const uint32_t sb = static_cast<uint32_t>((it & 1) * S::SB);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s8 a[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = tr8(sb + a_l + 2 * i * S::DPL + 512 * ks, sb + a_l + 2 * i * S::DPL + 512 * ks + 256);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const uint32_t toff = static_cast<uint32_t>(((t / 3) * S::RS + (t % 3)) * 16);
+        const s8 b = tr8(sb + b_l[ks][0] + toff, sb + b_l[ks][1] + toff);
+        acc[t][0] = mfma(a[0], b, acc[t][0]);
+        acc[t][1] = mfma(a[1], b, acc[t][1]);
+      }
+    }
+  }
+  // acc[t][i][r] = partial dW[co = cot*64 + 32 wco + 16 i + 4 lg + r][tap t][ci = cb*64 + 16 cig + i16]
+  const int64_t Ktot = 9LL * g.C;
+  float* dst = part + static_cast<int64_t>(split) * g.K * Ktot;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t co = static_cast<int64_t>(cot) * 64 + 32 * wco + 16 * i + 4 * lg + r;
+        dst[co * Ktot + t * g.C + cb * 64 + 16 * cig + i16] = acc[t][i][r];
+      }
+}
+
 // ------------------------------------------------------------------------------------------ host
 struct V2Cfg {
   int W, TR, bco, wco, nb, res;
@@ -769,6 +936,72 @@ int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, in
   }
 #undef V2E
 #undef V2L
+  return 0;
+}
+
+// ---- weight gradient: 224 lane pixels (7 k-steps) per stage -- cfg 0: 56x56 layers, 4-row stages; 1: 28x28,
+// 7 rows padded to 32 lanes; 2: 14x14, whole images padded to 16 lanes
+namespace {
+struct V2WCfg {
+  int W, TR, WR;
+};
+constexpr V2WCfg kV2W[] = {{56, 4, 56}, {28, 7, 32}, {14, 14, 16}};
+int v2w_lds(int cfg) {
+  switch (cfg) {
+    case 0: return WShape<56, 4, 56>::LDS;
+    case 1: return WShape<28, 7, 32>::LDS;
+    default: return WShape<14, 14, 16>::LDS;
+  }
+}
+}  // namespace
+
+int damd_v2w_num_cfgs() { return static_cast<int>(sizeof(kV2W) / sizeof(kV2W[0])); }
+
+int damd_v2w_supported(int C, int K, int H, int W, int cfg) {
+  if (cfg < 0 || cfg >= damd_v2w_num_cfgs()) return 0;
+  const V2WCfg c = kV2W[cfg];
+  return W == c.W && H > 0 && H % c.TR == 0 && C > 0 && C % 64 == 0 && K > 0 && K % 64 == 0 &&
+         v2w_lds(cfg) <= 160 * 1024;
+}
+
+// partial-sum slabs of a launch (= pixel splits): about one block per CU over all (co, ci) tiles
+int damd_v2w_splits(int64_t N, int H, int C, int K, int cfg) {
+  const int64_t tiles = static_cast<int64_t>(K / 64) * (C / 64);
+  const int64_t stages = N * (H / kV2W[cfg].TR);
+  int64_t sp = (256 + tiles - 1) / tiles;
+  if (sp > stages / 2) sp = stages / 2;
+  return static_cast<int>(sp < 1 ? 1 : sp);
+}
+
+// x: [N, H, W, C]; dy: [N, H, W, K]; part: [splits][K][9 C] fp32 (summed by the caller)
+int damd_v2w_launch(const void* x, const void* dy, float* part, int N, int H, int W, int C, int K, int cfg,
+                    int splits, hipStream_t st) {
+  if (!damd_v2w_supported(C, K, H, W, cfg)) return -1;
+  const V2WCfg c = kV2W[cfg];
+  if (static_cast<int64_t>(N) * H * W * (C > K ? C : K) >= (int64_t{1} << 31) - 4096) return -7;
+  if (splits != damd_v2w_splits(N, H, C, K, cfg)) return -5;
+  WGeo g;
+  g.N = N; g.H = H; g.C = C; g.K = K;
+  g.cotiles = K / 64;
+  g.cblks = C / 64;
+  g.splits = splits;
+  g.stages = N * (H / c.TR);
+  const dim3 grid(static_cast<unsigned>(g.cotiles * g.cblks * splits));
+  const int lds = v2w_lds(cfg);
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* dp = static_cast<const bf16_t*>(dy);
+#define V2W(W_, TR_, WR_)                                                                                    \
+  do {                                                                                                       \
+    auto* kfn = conv3x3v2_wgrad_kernel<W_, TR_, WR_>;                                                           \
+    DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    DAMD_LAUNCH(kfn, grid, dim3(512), lds, st, xp, dp, part, g);                                              \
+  } while (0)
+  switch (cfg) {
+    case 0: V2W(56, 4, 56); break;
+    case 1: V2W(28, 7, 32); break;
+    default: V2W(14, 14, 16); break;
+  }
+#undef V2W
   return 0;
 }
 

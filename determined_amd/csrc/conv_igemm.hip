@@ -2092,22 +2092,34 @@ int damd_wgrad_launch(const void* x, const void* dy, float* part, void* dw, int 
 }  // extern "C"
 
 
-// ---- 3x3 halo weight gradient (cfg 0: 128 output channels per block, 1: 64)
+// ---- 3x3 halo weight gradient (cfg 0: 128 output channels per block, 1: 64; cfg 2 + k: conv3x3v2.hip's
+// whole-row-tile kernel, its config k)
+extern "C" int damd_v2w_num_cfgs();
+extern "C" int damd_v2w_supported(int C, int K, int H, int W, int cfg);
+extern "C" int damd_v2w_splits(int64_t N, int H, int C, int K, int cfg);
+extern "C" int damd_v2w_launch(const void* x, const void* dy, float* part, int N, int H, int W, int C, int K, int cfg,
+                               int splits, hipStream_t st);
 namespace {
 int hw_bco(int cfg) { return cfg == 0 ? 128 : 64; }
 int hw_halo_rows(int W) { return (kHwPB + 2 * (W + 1) + 2 + 7) / 8 * 8; }
 int hw_lds_bytes(int bco, int W) { return 2 * (2 * (bco / 64) * 64 * 64 + hw_halo_rows(W) * 64) * 2; }
+int hw_launch(const void* x, const void* dy, float* part, int N, int H, int W, int C, int K, int cfg, int splits,
+              hipStream_t st);
 }  // namespace
 
 extern "C" {
 
-int damd_wgrad3x3_supported(int C, int K, int W, int cfg) {
+int damd_wgrad3x3_num_cfgs() { return 2 + damd_v2w_num_cfgs(); }
+
+int damd_wgrad3x3_supported(int C, int K, int H, int W, int cfg) {
+  if (cfg >= 2) return damd_v2w_supported(C, K, H, W, cfg - 2);
   if (cfg < 0 || cfg > 1) return 0;
   const int bco = hw_bco(cfg);
   return C % 64 == 0 && K % bco == 0 && W >= 1 && hw_lds_bytes(bco, W) <= 160 * 1024;
 }
 
 int damd_wgrad3x3_splits(int64_t N, int H, int W, int C, int K, int cfg, int splits_override) {
+  if (cfg >= 2) return damd_v2w_splits(N, H, C, K, cfg - 2);
   const int64_t tiles = static_cast<int64_t>(K / hw_bco(cfg)) * (C / 64);
   int64_t splits = splits_override > 0 ? splits_override : (256 + tiles - 1) / tiles;
   const int64_t Mp = N * (H + 1) * (W + 1);
@@ -2120,7 +2132,29 @@ int damd_wgrad3x3_splits(int64_t N, int H, int W, int C, int K, int cfg, int spl
 // x: [N, H, W, C]; dy: [N, H, W, K] (stride 1, pad 1); part: [splits][K][9*C] fp32; dw: [K][3][3][C]
 int damd_wgrad3x3_launch(const void* x, const void* dy, float* part, void* dw, int w_dtype, int N, int H, int W,
                          int C, int K, int cfg, int splits, hipStream_t st) {
-  if (!damd_wgrad3x3_supported(C, K, W, cfg)) return -1;
+  if (!damd_wgrad3x3_supported(C, K, H, W, cfg)) return -1;
+  if (cfg >= 2) {
+    const int rc = damd_v2w_launch(x, dy, part, N, H, W, C, K, cfg - 2, splits, st);
+    if (rc != 0) return rc;
+  } else {
+    const int rc = hw_launch(x, dy, part, N, H, W, C, K, cfg, splits, st);
+    if (rc != 0) return rc;
+  }
+  const int64_t n = static_cast<int64_t>(K) * 9 * C;
+  const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
+  if (w_dtype == 1)
+    DAMD_LAUNCH(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
+  else
+    DAMD_LAUNCH(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
+  DAMD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+int hw_launch(const void* x, const void* dy, float* part, int N, int H, int W, int C, int K, int cfg, int splits,
+              hipStream_t st) {
   const int64_t Mp = static_cast<int64_t>(N) * (H + 1) * (W + 1);
   if (Mp >= (int64_t{1} << 31) - 4096) return -2;
   const int bco = hw_bco(cfg);
@@ -2147,17 +2181,9 @@ int damd_wgrad3x3_launch(const void* x, const void* dy, float* part, void* dw, i
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DAMD_LAUNCH(conv3x3_wgrad_kernel<64>, grid, dim3(512), lds, st, xp, dp, part, g);
   }
-  const int64_t n = static_cast<int64_t>(K) * 9 * C;
-  const dim3 fg(static_cast<unsigned>((n / 4 + 63) / 64));
-  if (w_dtype == 1)
-    DAMD_LAUNCH(wgrad_finalize_kernel<bf16_t>, fg, dim3(256), 0, st, part, splits, n, static_cast<bf16_t*>(dw));
-  else
-    DAMD_LAUNCH(wgrad_finalize_kernel<float>, fg, dim3(256), 0, st, part, splits, n, static_cast<float*>(dw));
-  DAMD_CHECK_LAUNCH();
   return 0;
 }
-
-}  // extern "C"
+}  // namespace
 
 
 // ---- fused 1x1 backward (K = 256 -> C = 64)

@@ -487,8 +487,9 @@ def _dgrad_s2_phases(e, dy: torch.Tensor, w: torch.Tensor, xshape, cfg: int) -> 
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
-    """Weight gradient: conv_igemm.hip's split-pixel kernel, its 3x3 halo kernel (stride-1 3x3) or
-    MIOpen, whichever timed faster for this shape."""
+    """Weight gradient: conv_igemm.hip's split-pixel kernel, the 3x3 halo kernels (stride-1 3x3:
+    conv_igemm.hip's pixel-run kernel "h0"/"h1", conv3x3v2.hip's whole-row-tile kernel "h2".."h4") or MIOpen,
+    whichever timed faster for this shape."""
     from determined_amd import ops
 
     e = ops.ext()
@@ -501,8 +502,8 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
     for c in range(e.wgrad_num_cfgs()):
         if e.wgrad_supported(x, dy, w.shape[0], c):
             cands[c] = (lambda c=c: e.conv_wgrad(x, dy, w, stride, pad, c, 0))
-    if stride == 1 and pad == 1 and w.shape[2] == 3 and w.shape[3] == 3:  # 3x3 halo kernel
-        for c in (0, 1):
+    if stride == 1 and pad == 1 and w.shape[2] == 3 and w.shape[3] == 3:  # 3x3 halo kernels
+        for c in range(e.wgrad3x3_num_cfgs()):
             if e.wgrad3x3_supported(x, dy, w, c):
                 cands[f"h{c}"] = (lambda c=c: e.conv3x3_wgrad(x, dy, w, c, 0))
     cands["miopen"] = miopen

@@ -71,6 +71,8 @@ class ModelArguments:
     stock_kernels: bool = False
     hidden_dropout_prob: float = 0.1
     attention_probs_dropout_prob: float = 0.1
+    # bf16 parameters with fp32 master weights inside the fused AdamW (no per-step autocast weight casts)
+    bf16_weights: bool = False
 
 
 def dict2args(d: Dict[str, Any]) -> List[str]:
@@ -96,6 +98,8 @@ def build_model(m: ModelArguments, bf16: bool) -> torch.nn.Module:
     model = transformers.BertForMaskedLM(cfg)
     if not m.stock_kernels:
         accelerate(model)
+    if m.bf16_weights:
+        model = model.to(torch.bfloat16)
     return model
 
 

@@ -3,7 +3,8 @@
 bf16 autocast as the HF Trainer runs it with ``--bf16``): the step the Trainer executes
 (forward, loss, backward, optimizer step, zero_grad) timed in a plain loop so the number is not
 diluted by the Trainer's logging.  Variants: ``fused`` (determined_amd.transformers.accelerate +
-fused AdamW) and ``stock`` (HF SDPA attention + torch fused AdamW).  One JSON line per variant.
+fused AdamW), ``fused_bf16w`` (the same with bf16 parameters and fp32 master weights in the fused AdamW:
+no per-step autocast weight casts) and ``stock`` (HF SDPA attention + torch fused AdamW).  One JSON line per variant.
 
     python scripts/bert_bench.py [--batch 64] [--seq 128] [--steps 30] [--warmup 10] [--variants fused,stock]
 """
@@ -27,11 +28,13 @@ def build(variant: str, seq: int, dropout: float):
                                   attention_probs_dropout_prob=dropout, attn_implementation="sdpa")
     torch.manual_seed(0)
     model = transformers.BertForMaskedLM(cfg).cuda()
-    if variant == "fused":
+    if variant in ("fused", "fused_bf16w"):
         accelerate(model)
         from determined_amd.ops import FusedAdamW
 
-        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
+        if variant == "fused_bf16w":  # bf16 parameters, fp32 master weights in the optimizer
+            model = model.to(torch.bfloat16)
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, master_weights=variant == "fused_bf16w")
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
     return model, opt
@@ -44,7 +47,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dropout", type=float, default=0.1)
-    ap.add_argument("--variants", default="fused,stock")
+    ap.add_argument("--variants", default="fused,fused_bf16w,stock")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     ids = torch.randint(1000, 30522, (a.batch, a.seq), device="cuda", generator=g)

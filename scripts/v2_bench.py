@@ -2,7 +2,8 @@
 """Per-config timing of the ResNet-50 3x3 stride-1 layers at the bench batch: every conv config that
 serves the layer (conv_igemm.hip generic / halo, conv3x3v2.hip padded-halo) for the forward with BN
 statistics, the BN+ReLU-prologue forward, the input gradient with the BN-backward epilogue, and the
-same with the deferred BN-backward apply prologue.  One JSON line per (layer, pass, config).
+same with the deferred BN-backward apply prologue, and the weight gradient.  One JSON line per (layer, pass,
+config).
 
     python scripts/v2_bench.py [--batch 2048] [--out gpurun_out/v2_bench.jsonl]
 """
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--out", default="gpurun_out/v2_bench.jsonl")
     ap.add_argument("--layers", default="64x56,128x28,256x14")
+    ap.add_argument("--passes", default="fwd_stats,fwd_bnrelu_pro,dgrad_bn_epi,dgrad_bn_epi_pro2,wgrad")
     a = ap.parse_args()
     from determined_amd import ops
 
@@ -67,6 +69,8 @@ def main():
             "dgrad_bn_epi_pro2": lambda k: e.conv_dgrad_bn(x, wt, 1, k, None, x, None, stats, yn, coef),
         }
         for pname, fn in passes.items():
+            if pname not in a.passes.split(","):
+                continue
             for k in cfgs:
                 if pname in ("fwd_bnrelu_pro", "dgrad_bn_epi_pro2") and not e.conv_pro_supported(x, w, k):
                     continue
@@ -80,6 +84,27 @@ def main():
                 out.write(json.dumps(rec) + "\n")
                 out.flush()
                 print(json.dumps(rec), flush=True)
+        # weight gradient: conv_igemm.hip's split-pixel configs, the 3x3 halo kernels ("h<cfg>": h0 / h1
+        # conv_igemm.hip, h2.. conv3x3v2.hip) and MIOpen
+        dyw = yn
+        wg = {f"w{k}": (lambda k=k: e.conv_wgrad(x, dyw, w, 1, 1, k, 0))
+              for k in range(e.wgrad_num_cfgs()) if e.wgrad_supported(x, dyw, w.shape[0], k)}
+        wg.update({f"h{k}": (lambda k=k: e.conv3x3_wgrad(x, dyw, w, k, 0))
+                   for k in range(e.wgrad3x3_num_cfgs()) if e.wgrad3x3_supported(x, dyw, w, k)})
+        wg["miopen"] = lambda: torch.ops.aten.convolution_backward(dyw, x, w, None, [1, 1], [1, 1], [1, 1], False,
+                                                                   [0, 0], 1, [False, True, False])[1]
+        for k, fn in (wg.items() if "wgrad" in a.passes.split(",") else ()):
+            try:
+                us = timeit(fn)
+            except RuntimeError as err:
+                print(f"{spec} wgrad {k}: {err}", flush=True)
+                continue
+            v2 = k.startswith("h") and int(k[1:]) >= 2
+            rec = {"layer": spec, "batch": n, "pass": "wgrad", "cfg": k, "v2": v2, "us": round(us, 1),
+                   "tflops": round(flops / us / 1e6, 1)}
+            out.write(json.dumps(rec) + "\n")
+            out.flush()
+            print(json.dumps(rec), flush=True)
         del x, w, wt, a_, yn
         torch.cuda.empty_cache()
 

@@ -56,6 +56,11 @@ def test_bert_base_mlm_bf16_fused_follows_fp32(monkeypatch):
     for i, (a, b) in enumerate(zip(fused, ref)):
         assert abs(a - b) <= 0.02 * abs(b) + 0.02, (i, fused, ref)
     assert fused[-1] < fused[0]
+    # bf16 parameters with fp32 master weights in the fused AdamW (--bf16_weights)
+    bw = _train(monkeypatch, ["--bf16", "true", "--bf16_weights", "true"] + nodrop)
+    assert len(bw) == 8
+    for i, (a, b) in enumerate(zip(bw, ref)):
+        assert abs(a - b) <= 0.03 * abs(b) + 0.03, (i, bw, ref)
 
 
 def test_bert_base_mlm_with_dropout_trains_like_without(monkeypatch):

@@ -144,3 +144,26 @@ def test_v2_refuses_unsupported_geometry(ext):
         assert not any(ext.conv_supported(x, w, c, 1, 1) for c in range(base, ext.conv_num_cfgs()))
     x = _rand(1, 64, 56, 56)
     assert not any(ext.conv_supported(x, w, c, 2, 1) for c in range(base, ext.conv_num_cfgs()))
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56), (1, 128, 64, 8, 56), (2, 128, 128, 28, 28),
+                                   (1, 64, 192, 14, 28), (2, 256, 128, 14, 14), (3, 64, 64, 14, 14)])
+def test_v2_wgrad_matches_fp32(ext, shape):
+    """conv3x3v2.hip's whole-row-tile weight gradient (wgrad3x3 cfgs >= 2: transposed LDS reads of
+    8-channel planes, zero border from out-of-range DMA offsets) vs fp32, bf16 and fp32 weight outputs,
+    run-to-run identical (deterministic split reduction)."""
+    n, cin, cout, h, wd = shape
+    torch.manual_seed(11)
+    x = _rand(n, cin, h, wd)
+    dy = _rand(n, cout, h, wd)
+    w = _rand(cout, cin, 3, 3)
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), stride=1, padding=1)
+    cfgs = [c for c in range(2, ext.wgrad3x3_num_cfgs()) if ext.wgrad3x3_supported(x, dy, w, c)]
+    assert cfgs, "shape not served by a v2 weight-gradient config"
+    for cfg in cfgs:
+        dw = ext.conv3x3_wgrad(x, dy, w, cfg, 0)
+        assert dw.shape == w.shape and dw.dtype == w.dtype and dw.is_contiguous(memory_format=CL)
+        torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+        dw32 = ext.conv3x3_wgrad(x, dy, w.float(), cfg, 0)
+        torch.testing.assert_close(dw32, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+        assert torch.equal(ext.conv3x3_wgrad(x, dy, w.float(), cfg, 0), dw32)
