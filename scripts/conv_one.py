@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Run one implicit-GEMM conv launch config repeatedly (for rocprofv3 PMC passes).
 
-    python scripts/conv_one.py CIN COUT K STRIDE HW CFG [--batch 512] [--iters 20] [--mode fwd|dgrad_bn]
+    python scripts/conv_one.py CIN COUT K STRIDE HW CFG [--batch 512] [--iters 20] [--mode fwd|dgrad_bn_pro|wgrad3x3]
+
+``--mode wgrad3x3``: the 3x3 stride-1 weight gradient, CFG = wgrad3x3 config (0/1 conv_igemm.hip, 2.. conv3x3v2.hip).
 """
 import argparse
 import os
@@ -16,7 +18,7 @@ for n in ("cin", "cout", "k", "stride", "hw", "cfg"):
     ap.add_argument(n, type=int)
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--iters", type=int, default=20)
-ap.add_argument("--mode", default="fwd", choices=["fwd", "dgrad_bn_pro"])
+ap.add_argument("--mode", default="fwd", choices=["fwd", "dgrad_bn_pro", "wgrad3x3"])
 a = ap.parse_args()
 from determined_amd import ops  # noqa: E402
 
@@ -25,6 +27,14 @@ cl = torch.channels_last
 x = torch.randn(a.batch, a.cin, a.hw, a.hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
 w = torch.randn(a.cout, a.cin, a.k, a.k, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
 pad = a.k // 2
+if a.mode == "wgrad3x3":
+    dy = torch.randn(a.batch, a.cout, a.hw, a.hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    assert a.k == 3 and a.stride == 1 and e.wgrad3x3_supported(x, dy, w, a.cfg)
+    for _ in range(a.iters):
+        e.conv3x3_wgrad(x, dy, w, a.cfg, 0)
+    torch.cuda.synchronize()
+    print("ok")
+    sys.exit(0)
 assert e.conv_supported(x, w, a.cfg, a.stride, pad)
 if a.mode == "dgrad_bn_pro":
     # 1x1 input gradient of a chained ResNet block: operand dy = A*dz + B*y + Cc formed in the
