@@ -688,12 +688,16 @@ struct WGeo {
   int cotiles, cblks, splits, stages;  // stages = N * H / TR
 };
 
-template <int W, int TR, int WR>
+// RG = 0: both images by LDS-DMA (lane-linear 1 KiB writes: each lane fetches 16 bytes of a different pixel,
+// 8x the cache-line traffic of the bytes used); RG = 1: register-staged with 8 consecutive lanes per pixel
+// (one 128-byte line), ds_write_b128 into the planes, loaded at the top of a stage and written mid-stage.
+template <int W, int TR, int WR, int RG>
 __global__ void __launch_bounds__(512, 1)
 conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ part,
                        WGeo g) {
   using S = WShape<W, TR, WR>;
   constexpr int KS = S::KS;
+  constexpr int NXC = (S::NXS * 8 + 511) / 512, NDC = (S::P * 8 + 511) / 512;  // RG: chunks per thread
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -735,6 +739,57 @@ conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ 
   }
   const uint32_t xbytes = static_cast<uint32_t>(((TR + 2) * W + 1) * g.C * 2);
   const uint32_t dbytes = static_cast<uint32_t>(TR * W * g.K * 2);
+  // ---- RG staging roles: chunk u = tid + 512 i -> (slot or pixel u >> 3, 8-channel plane u & 7)
+  uint32_t rxo[RG ? NXC : 1], rdo[RG ? NDC : 1];
+  uint32_t rxok = 0, rxtop = 0, rxbot = 0, rdok = 0, rxin = 0, rdin = 0;
+  if (RG) {
+#pragma unroll
+    for (int i = 0; i < NXC; ++i) {
+      const int u = tid + 512 * i, slot = u >> 3, c = u & 7;
+      const int hr = slot / S::RS, wc = slot - (slot / S::RS) * S::RS;
+      const bool in = slot < S::HS;
+      rxo[i] = static_cast<uint32_t>(((hr * W + wc) * g.C + c * 8) * 2);
+      rxok |= (in && wc >= 1 && wc <= W ? 1u : 0u) << i;
+      rxtop |= (in && hr == 0 ? 1u : 0u) << i;
+      rxbot |= (in && hr == TR + 1 ? 1u : 0u) << i;
+      rxin |= (slot < S::NXS ? 1u : 0u) << i;
+    }
+#pragma unroll
+    for (int i = 0; i < NDC; ++i) {
+      const int u = tid + 512 * i, p = u >> 3, c = u & 7;
+      const int row = p / S::WR, col = p - (p / S::WR) * S::WR;
+      rdo[i] = static_cast<uint32_t>(((row * W + col) * g.K + c * 8) * 2);
+      rdok |= (p < S::P && col < W ? 1u : 0u) << i;
+      rdin |= (p < S::P ? 1u : 0u) << i;
+    }
+  }
+  const uint32_t rxl = static_cast<uint32_t>((tid & 7) * S::XPL + (tid >> 3) * 16);
+  const uint32_t rdl = static_cast<uint32_t>(S::XB + (tid & 7) * S::DPL + (tid >> 3) * 16);
+  u32x4 rxv[RG ? NXC : 1], rdv[RG ? NDC : 1];
+  auto rg_load = [&](int st) __attribute__((always_inline)) {
+    const int n = st / tiles_per_img, h0 = (st - n * tiles_per_img) * TR;
+    const int64_t pix0 = (static_cast<int64_t>(n) * g.H + h0) * W;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(x + (pix0 - (W + 1)) * g.C + cb * 64), 0, static_cast<int>(xbytes), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(dy + pix0 * g.K + cot * 64), 0, static_cast<int>(dbytes), 0x00020000);
+    const uint32_t okm = rxok & (h0 == 0 ? ~rxtop : ~0u) & (h0 + TR == g.H ? ~rxbot : ~0u);
+#pragma unroll
+    for (int i = 0; i < NXC; ++i)
+      rxv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, (okm >> i) & 1u ? rxo[i] : 0x80000000u, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NDC; ++i)
+      rdv[i] = __builtin_amdgcn_raw_buffer_load_b128(rd, (rdok >> i) & 1u ? rdo[i] : 0x80000000u, 0, 0);
+  };
+  auto rg_write = [&](int buf) __attribute__((always_inline)) {
+    char* b = lds + buf * S::SB;
+#pragma unroll
+    for (int i = 0; i < NXC; ++i)
+      if ((rxin >> i) & 1u) *reinterpret_cast<u32x4*>(b + rxl + 1024 * i) = rxv[i];
+#pragma unroll
+    for (int i = 0; i < NDC; ++i)
+      if ((rdin >> i) & 1u) *reinterpret_cast<u32x4*>(b + rdl + 1024 * i) = rdv[i];
+  };
   auto issue = [&](int st, int buf) __attribute__((always_inline)) {
     const int n = st / tiles_per_img, h0 = (st - n * tiles_per_img) * TR;
     const int64_t pix0 = (static_cast<int64_t>(n) * g.H + h0) * W;
@@ -779,14 +834,29 @@ conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ 
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f4{0.f, 0.f, 0.f, 0.f};
 
-  if (items > 0) issue(s_begin, 0);
+  if (items > 0) {
+    if (RG) {
+      rg_load(s_begin);
+      rg_write(0);
+    } else {
+      issue(s_begin, 0);
+    }
+  }
   for (int it = 0; it < items; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (RG) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();  // stage it landed for every wave; stage it-1 is no longer read
-    if (it + 1 < items) issue(s_begin + it + 1, (it + 1) & 1);
+    if (it + 1 < items) {
+      if (RG) rg_load(s_begin + it + 1);
+      else issue(s_begin + it + 1, (it + 1) & 1);
+    }
     const uint32_t sb = static_cast<uint32_t>((it & 1) * S::SB);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      if (RG && ks == KS / 2 && it + 1 < items) rg_write((it + 1) & 1);  // the other buffer: free since the barrier
       s8 a[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -945,9 +1015,10 @@ namespace {
 struct V2WCfg {
   int W, TR, WR;
 };
-constexpr V2WCfg kV2W[] = {{56, 4, 56}, {28, 7, 32}, {14, 14, 16}};
+// cfg 3 .. 5: the same with register-staged, line-coalesced loads (RG = 1)
+constexpr V2WCfg kV2W[] = {{56, 4, 56}, {28, 7, 32}, {14, 14, 16}, {56, 4, 56}, {28, 7, 32}, {14, 14, 16}};
 int v2w_lds(int cfg) {
-  switch (cfg) {
+  switch (cfg % 3) {
     case 0: return WShape<56, 4, 56>::LDS;
     case 1: return WShape<28, 7, 32>::LDS;
     default: return WShape<14, 14, 16>::LDS;
@@ -990,16 +1061,19 @@ int damd_v2w_launch(const void* x, const void* dy, float* part, int N, int H, in
   const int lds = v2w_lds(cfg);
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* dp = static_cast<const bf16_t*>(dy);
-#define V2W(W_, TR_, WR_)                                                                                    \
+#define V2W(W_, TR_, WR_, RG_)                                                                               \
   do {                                                                                                       \
-    auto* kfn = conv3x3v2_wgrad_kernel<W_, TR_, WR_>;                                                           \
+    auto* kfn = conv3x3v2_wgrad_kernel<W_, TR_, WR_, RG_>;                                                           \
     DAMD_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     DAMD_LAUNCH(kfn, grid, dim3(512), lds, st, xp, dp, part, g);                                              \
   } while (0)
   switch (cfg) {
-    case 0: V2W(56, 4, 56); break;
-    case 1: V2W(28, 7, 32); break;
-    default: V2W(14, 14, 16); break;
+    case 0: V2W(56, 4, 56, 0); break;
+    case 1: V2W(28, 7, 32, 0); break;
+    case 2: V2W(14, 14, 16, 0); break;
+    case 3: V2W(56, 4, 56, 1); break;
+    case 4: V2W(28, 7, 32, 1); break;
+    default: V2W(14, 14, 16, 1); break;
   }
 #undef V2W
   return 0;
