@@ -488,8 +488,8 @@ def _dgrad_s2_phases(e, dy: torch.Tensor, w: torch.Tensor, xshape, cfg: int) -> 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
     """Weight gradient: conv_igemm.hip's split-pixel kernel, the 3x3 halo kernels (stride-1 3x3:
-    conv_igemm.hip's pixel-run kernel "h0"/"h1", conv3x3v2.hip's whole-row-tile kernel "h2".."h4") or MIOpen,
-    whichever timed faster for this shape."""
+    conv_igemm.hip's pixel-run kernel "h0"/"h1", conv3x3v2.hip's whole-row-tile kernels "h2".."h7"), one
+    hipBLASLt GEMM for a stride-1 1x1 conv ("gemm") or MIOpen, whichever timed faster for this shape."""
     from determined_amd import ops
 
     e = ops.ext()
@@ -506,6 +506,16 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad:
         for c in range(e.wgrad3x3_num_cfgs()):
             if e.wgrad3x3_supported(x, dy, w, c):
                 cands[f"h{c}"] = (lambda c=c: e.conv3x3_wgrad(x, dy, w, c, 0))
+    if stride in (1, 2) and pad == 0 and w.shape[2] == 1 and w.shape[3] == 1 and x.dtype == dy.dtype:
+        # a 1x1 weight gradient is one GEMM over the output pixels, dW[K, C] = dY^T X (hipBLASLt); stride 2
+        # takes the even pixels of X (one gathering copy)
+        def gemm():
+            cout, cin = w.shape[0], w.shape[1]
+            d2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            xs = x if stride == 1 else x[:, :, ::2, ::2]
+            x2 = xs.permute(0, 2, 3, 1).reshape(-1, cin)
+            return (d2.t() @ x2).to(w.dtype).view(cout, cin, 1, 1)
+        cands["gemm"] = gemm
     cands["miopen"] = miopen
     key = ("wgrad", tuple(x.shape), tuple(w.shape), stride, pad)
     return cands[_pick(key, cands, default="miopen")]()

@@ -198,3 +198,26 @@ def test_conv_fwd_input_over_2gib(ext, k, st):
             torch.testing.assert_close(y[lo:lo + 8].float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
         del y
     torch.cuda.empty_cache()
+
+
+def test_1x1_wgrad_gemm_candidate_matches_fp32(ext, monkeypatch):
+    """The hipBLASLt candidate of the 1x1 stride-1 weight gradient (dW = dY^T X over the pixels)
+    against fp32, in the layout and dtype of the other candidates."""
+    from determined_amd.ops import conv as C
+
+    torch.manual_seed(3)
+    x = cl(torch.randn(4, 128, 14, 14, device="cuda").to(torch.bfloat16))
+    dy = cl(torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16))
+    w = cl(torch.randn(256, 128, 1, 1, device="cuda").to(torch.bfloat16))
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), stride=1, padding=0)
+    picked = []
+    monkeypatch.setattr(C, "_pick", lambda key, cands, default=None: picked.append(sorted(map(str, cands))) or "gemm")
+    dw = C._wgrad(dy, x, w, 1, 0)
+    assert "gemm" in picked[0]
+    assert dw.shape == w.shape and dw.dtype == w.dtype and dw.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    # stride 2 (the downsample shortcut): the even pixels of x
+    dy2 = cl(torch.randn(4, 256, 7, 7, device="cuda").to(torch.bfloat16))
+    ref2 = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy2.float(), stride=2, padding=0)
+    dw2 = C._wgrad(dy2, x, w, 2, 0)
+    torch.testing.assert_close(dw2.float(), ref2, rtol=2e-2, atol=2e-2 * ref2.abs().max().item())
