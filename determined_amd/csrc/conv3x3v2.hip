@@ -669,11 +669,13 @@ constexpr int wpitch(int b) { return b <= 128 ? 128 : (b - 128 + 255) / 256 * 25
 template <int W, int TR, int WR_>
 struct WShape {
   static constexpr int WR = WR_;               // lane pixels per image row (>= W, a multiple of 4)
-  static constexpr int P = TR * WR;            // lane pixels per stage
+  static constexpr int PV = TR * WR;           // lane pixels of the stage's rows
+  static constexpr int P = (PV + 31) / 32 * 32;  // lane pixels per stage (pixels >= PV: zero dY)
   static constexpr int KS = P / 32;            // k-steps per stage
   static constexpr int RS = W + 2, HS = (TR + 2) * RS;
-  static constexpr int XS = WR + 2 > RS ? WR + 2 - RS : 0;  // slots past HS that pad pixels' taps read
-  static constexpr int XPL = wpitch((HS + XS) * 16);        // x halo plane pitch (8 channels)
+  // slots the taps of every lane pixel read (pad pixels' reads past HS hit zeros or finite data times zero dY)
+  static constexpr int XR = ((P - 1) / WR + 2) * RS + WR + 2;
+  static constexpr int XPL = wpitch((XR > HS ? XR : HS) * 16);  // x halo plane pitch (8 channels)
   static constexpr int DPL = wpitch(P * 16);                // dY plane pitch
   static constexpr int XB = 8 * XPL, SB = XB + 8 * DPL;     // x image / stage bytes
   static constexpr int LDS = 2 * SB;
@@ -735,7 +737,7 @@ conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ 
     const int p = bd0(b) + lane;
     const int row = p / S::WR, col = p - (p / S::WR) * S::WR;
     dof[b] = static_cast<uint32_t>(((row * W + col) * g.K + wave * 8) * 2);
-    dok |= (col < W ? 1u : 0u) << b;
+    dok |= (p < S::PV && col < W ? 1u : 0u) << b;
   }
   const uint32_t xbytes = static_cast<uint32_t>(((TR + 2) * W + 1) * g.C * 2);
   const uint32_t dbytes = static_cast<uint32_t>(TR * W * g.K * 2);
@@ -759,7 +761,7 @@ conv3x3v2_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ 
       const int u = tid + 512 * i, p = u >> 3, c = u & 7;
       const int row = p / S::WR, col = p - (p / S::WR) * S::WR;
       rdo[i] = static_cast<uint32_t>(((row * W + col) * g.K + c * 8) * 2);
-      rdok |= (p < S::P && col < W ? 1u : 0u) << i;
+      rdok |= (p < S::PV && col < W ? 1u : 0u) << i;
       rdin |= (p < S::P ? 1u : 0u) << i;
     }
   }
@@ -1010,14 +1012,17 @@ int damd_v2_launch(const void* x, const void* w, void* y, float* part, int N, in
 }
 
 // ---- weight gradient: 224 lane pixels (7 k-steps) per stage -- cfg 0: 56x56 layers, 4-row stages; 1: 28x28,
-// 7 rows padded to 32 lanes; 2: 14x14, whole images padded to 16 lanes
+// 7 rows padded to 32 lanes; 2: 14x14, whole images padded to 16 lanes; 6: 7x7, whole images (8-lane rows,
+// 56 + 8 zero pixels: 2 k-steps)
 namespace {
 struct V2WCfg {
   int W, TR, WR;
 };
 // cfg 3 .. 5: the same with register-staged, line-coalesced loads (RG = 1)
-constexpr V2WCfg kV2W[] = {{56, 4, 56}, {28, 7, 32}, {14, 14, 16}, {56, 4, 56}, {28, 7, 32}, {14, 14, 16}};
+constexpr V2WCfg kV2W[] = {{56, 4, 56}, {28, 7, 32}, {14, 14, 16}, {56, 4, 56}, {28, 7, 32}, {14, 14, 16},
+                           {7, 7, 8}, {7, 7, 8}};
 int v2w_lds(int cfg) {
+  if (cfg >= 6) return WShape<7, 7, 8>::LDS;
   switch (cfg % 3) {
     case 0: return WShape<56, 4, 56>::LDS;
     case 1: return WShape<28, 7, 32>::LDS;
@@ -1035,11 +1040,14 @@ int damd_v2w_supported(int C, int K, int H, int W, int cfg) {
          v2w_lds(cfg) <= 160 * 1024;
 }
 
-// partial-sum slabs of a launch (= pixel splits): about one block per CU over all (co, ci) tiles
+// partial-sum slabs of a launch (= pixel splits): about as many blocks as fit on the 256 CUs at once (the
+// small 7x7 stages leave room for up to 3 blocks per CU) over all (co, ci) tiles
 int damd_v2w_splits(int64_t N, int H, int C, int K, int cfg) {
   const int64_t tiles = static_cast<int64_t>(K / 64) * (C / 64);
   const int64_t stages = N * (H / kV2W[cfg].TR);
-  int64_t sp = (256 + tiles - 1) / tiles;
+  int per_cu = 160 * 1024 / v2w_lds(cfg);
+  per_cu = per_cu < 1 ? 1 : per_cu > 3 ? 3 : per_cu;
+  int64_t sp = (256 * per_cu + tiles - 1) / tiles;
   if (sp > stages / 2) sp = stages / 2;
   return static_cast<int>(sp < 1 ? 1 : sp);
 }
@@ -1073,7 +1081,9 @@ int damd_v2w_launch(const void* x, const void* dy, float* part, int N, int H, in
     case 2: V2W(14, 14, 16, 0); break;
     case 3: V2W(56, 4, 56, 1); break;
     case 4: V2W(28, 7, 32, 1); break;
-    default: V2W(14, 14, 16, 1); break;
+    case 5: V2W(14, 14, 16, 1); break;
+    case 6: V2W(7, 7, 8, 0); break;
+    default: V2W(7, 7, 8, 1); break;
   }
 #undef V2W
   return 0;

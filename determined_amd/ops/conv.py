@@ -488,7 +488,7 @@ def _dgrad_s2_phases(e, dy: torch.Tensor, w: torch.Tensor, xshape, cfg: int) -> 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
     """Weight gradient: conv_igemm.hip's split-pixel kernel, the 3x3 halo kernels (stride-1 3x3:
-    conv_igemm.hip's pixel-run kernel "h0"/"h1", conv3x3v2.hip's whole-row-tile kernels "h2".."h7"), one
+    conv_igemm.hip's pixel-run kernel "h0"/"h1", conv3x3v2.hip's whole-row-tile kernels "h2".."h9"), one
     hipBLASLt GEMM for a stride-1 1x1 conv ("gemm") or MIOpen, whichever timed faster for this shape."""
     from determined_amd import ops
 

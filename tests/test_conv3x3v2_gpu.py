@@ -147,7 +147,8 @@ def test_v2_refuses_unsupported_geometry(ext):
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56), (1, 128, 64, 8, 56), (2, 128, 128, 28, 28),
-                                   (1, 64, 192, 14, 28), (2, 256, 128, 14, 14), (3, 64, 64, 14, 14)])
+                                   (1, 64, 192, 14, 28), (2, 256, 128, 14, 14), (3, 64, 64, 14, 14),
+                                   (3, 128, 64, 7, 7)])
 def test_v2_wgrad_matches_fp32(ext, shape):
     """conv3x3v2.hip's whole-row-tile weight gradient (wgrad3x3 cfgs >= 2: transposed LDS reads of
     8-channel planes, zero border from out-of-range DMA offsets) vs fp32, bf16 and fp32 weight outputs,
