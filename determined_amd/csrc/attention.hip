@@ -76,7 +76,12 @@ struct KeyMaskDrop {
   uint32_t seed;       // dropout stream
   uint32_t thresh;     // drop when hash < thresh (0: no dropout)
   float inv_keep;      // 1 / (1 - p)
+  const int64_t* seedp;  // device-side seed (read at run time: a graph-captured step draws a new one per replay)
 };
+
+__device__ __forceinline__ uint32_t md_seed(const KeyMaskDrop& md) {
+  return md.seedp != nullptr ? static_cast<uint32_t>(*md.seedp) : md.seed;
+}
 
 struct FwdArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
@@ -288,7 +293,7 @@ __global__ void __launch_bounds__(kThreads) attn_fwd_kernel(FwdArgs a) {
           const float p = ex2(fmaf(s[qt][nt][r], a.scale_log2, -m_use));
           rs += p;
           if constexpr (DROP)
-            s[qt][nt][r] = drop_keep(a.md.seed, a.md.thresh, bh32, myq, k0 + nt * 16 + 4 * g + r) ? p : 0.f;
+            s[qt][nt][r] = drop_keep(md_seed(a.md), a.md.thresh, bh32, myq, k0 + nt * 16 + 4 * g + r) ? p : 0.f;
           else
             s[qt][nt][r] = p;
         }
@@ -435,7 +440,7 @@ __global__ void __launch_bounds__(kThreads) attn_bwd_kernel(BwdArgs a) {
         float p = ex2(fmaf(sacc[r], a.scale_log2, -lse2[ql]));
         if (need_mask) p = (!kvalid || (CAUSAL && mykey > q0 + ql)) ? 0.f : p;
         if constexpr (DROP) {
-          const bool keep = drop_keep(a.md.seed, a.md.thresh, static_cast<uint32_t>(bh), q0 + ql, mykey);
+          const bool keep = drop_keep(md_seed(a.md), a.md.thresh, static_cast<uint32_t>(bh), q0 + ql, mykey);
           P[qt][r] = keep ? p * a.md.inv_keep : 0.f;  // dV uses the dropped, rescaled probabilities
           dS[qt][r] = p * ((keep ? dpacc[r] * a.md.inv_keep : 0.f) - dl[ql]);
         } else {
@@ -573,7 +578,7 @@ __global__ void __launch_bounds__(kThreads) attn_dq_kernel(DqArgs a) {
           p = ((mw >> (8 * r)) & 0xffu) ? p : 0.f;
           float dpv = dp[qt][nt][r];
           if constexpr (DROP)
-            dpv = drop_keep(a.md.seed, a.md.thresh, static_cast<uint32_t>(bh), myq, key) ? dpv * a.md.inv_keep : 0.f;
+            dpv = drop_keep(md_seed(a.md), a.md.thresh, static_cast<uint32_t>(bh), myq, key) ? dpv * a.md.inv_keep : 0.f;
           s[qt][nt][r] = p * (dpv - dl[qt]);  // dS^T
         }
       }
@@ -638,11 +643,12 @@ extern "C" {
     }                                                                                                \
   } while (0)
 
-static KeyMaskDrop make_md(const uint8_t* km, int64_t kms, uint32_t seed, float drop_p) {
+static KeyMaskDrop make_md(const uint8_t* km, int64_t kms, uint32_t seed, const int64_t* seedp, float drop_p) {
   KeyMaskDrop md;
   md.km = km;
   md.kms = kms;
   md.seed = seed;
+  md.seedp = seedp;
   const double t = static_cast<double>(drop_p) * 4294967296.0;
   md.thresh = drop_p > 0.f ? static_cast<uint32_t>(t >= 4294967295.0 ? 4294967295.0 : (t < 1.0 ? 1.0 : t)) : 0u;
   md.inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
@@ -652,14 +658,14 @@ static KeyMaskDrop make_md(const uint8_t* km, int64_t kms, uint32_t seed, float 
 // strides: 4 tensors (q, k, v, o) x (b, h, t) in elements; km: optional [B][kms] key mask
 void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
                           int B, int H, int T, int D, float scale, int causal, const uint8_t* km, int64_t kms,
-                          uint32_t seed, float drop_p, hipStream_t st) {
+                          uint32_t seed, const int64_t* seedp, float drop_p, hipStream_t st) {
   FwdArgs a;
   a.q = static_cast<const bf16_t*>(q); a.k = static_cast<const bf16_t*>(k); a.v = static_cast<const bf16_t*>(v);
   a.o = static_cast<bf16_t*>(o); a.lse = lse;
   a.sq = {strides[0], strides[1], strides[2]}; a.sk = {strides[3], strides[4], strides[5]};
   a.sv = {strides[6], strides[7], strides[8]}; a.so = {strides[9], strides[10], strides[11]};
   a.H = H; a.T = T; a.scale_log2 = scale * kLog2e;
-  a.md = make_md(km, kms, seed, drop_p);
+  a.md = make_md(km, kms, seed, seedp, drop_p);
   dim3 grid((T + kFwdRows - 1) / kFwdRows, H, B);
   DAMD_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
 }
@@ -668,7 +674,8 @@ void damd_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
 void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
                           const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
                           const int64_t* s, int B, int H, int T, int D, float scale, int causal,
-                          const uint8_t* km, int64_t kms, uint32_t seed, float drop_p, hipStream_t st) {
+                          const uint8_t* km, int64_t kms, uint32_t seed, const int64_t* seedp, float drop_p,
+                          hipStream_t st) {
   const Strides sq{s[0], s[1], s[2]}, sk{s[3], s[4], s[5]}, sv{s[6], s[7], s[8]}, so{s[9], s[10], s[11]},
       sdo{s[12], s[13], s[14]}, sdk{s[15], s[16], s[17]}, sdv{s[18], s[19], s[20]}, sdq{s[21], s[22], s[23]};
   const int64_t rows = static_cast<int64_t>(B) * H * T;
@@ -690,7 +697,7 @@ void damd_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   a.dk = static_cast<bf16_t*>(dk); a.dv = static_cast<bf16_t*>(dv);
   a.sq = sq; a.sk = sk; a.sv = sv; a.sdo = sdo; a.sdk = sdk; a.sdv = sdv;
   a.H = H; a.T = T; a.scale = scale; a.scale_log2 = scale * kLog2e;
-  a.md = make_md(km, kms, seed, drop_p);
+  a.md = make_md(km, kms, seed, seedp, drop_p);
   dim3 grid((T + kBlk - 1) / kBlk, H, B);
   DAMD_ATTN_DISPATCH(attn_bwd_kernel, grid, a);
   DqArgs d;

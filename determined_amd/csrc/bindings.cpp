@@ -54,7 +54,7 @@ int damd_norm_bwd_launch(const void*, const void*, const float*, const float*, c
 void damd_norm_wgrad_finalize_launch(const float*, const float*, int, int, void*, void*, int, hipStream_t);
 int damd_resid_norm_supported(int);
 void damd_resid_norm_fwd_launch(const void*, const void*, const void*, const void*, void*, void*, uint8_t*, float*,
-                                float*, int64_t, int, float, float, uint32_t, int, int, hipStream_t);
+                                float*, int64_t, int, float, float, uint32_t, const int64_t*, int, int, hipStream_t);
 int damd_resid_norm_bwd_launch(const void*, const void*, const void*, const float*, const float*, const void*,
                                const uint8_t*, float, void*, void*, float*, float*, int64_t, int, int, int,
                                hipStream_t);
@@ -172,10 +172,11 @@ extern "C" int damd_stem_wgrad_blocks(int64_t, int);
 extern "C" void damd_stem_wgrad_launch(const void*, const void*, float*, void*, int, int64_t, int, int, hipStream_t);
 // launchers (attention.hip)
 extern "C" void damd_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, int, int,
-                                     int, int, float, int, const uint8_t*, int64_t, uint32_t, float, hipStream_t);
+                                     int, int, float, int, const uint8_t*, int64_t, uint32_t, const int64_t*, float,
+                                     hipStream_t);
 extern "C" void damd_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*,
                                      float*, float*, void*, void*, void*, const int64_t*, int, int, int, int, float,
-                                     int, const uint8_t*, int64_t, uint32_t, float, hipStream_t);
+                                     int, const uint8_t*, int64_t, uint32_t, const int64_t*, float, hipStream_t);
 // launchers (fused.hip)
 extern "C" void damd_lm_ce_fwd_launch(const void*, const int64_t*, int64_t, int, int, int, int64_t, float*, float*,
                                       hipStream_t);
@@ -631,6 +632,14 @@ std::vector<at::Tensor> bn_bwd_from_part(const at::Tensor& dz, const at::Tensor&
 }
 
 // ---------------------------------------------------------------- residual add + dropout + LayerNorm
+// optional device-side dropout seed: a 1-element int64 tensor on x's device, read by the kernel at run time
+const int64_t* seed_ptr(const c10::optional<at::Tensor>& t, const at::Tensor& x) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() >= 1 && t->device() == x.device(),
+              "seed_t: int64 tensor on the input's device");
+  return t->data_ptr<int64_t>();
+}
+
 bool resid_norm_supported(const at::Tensor& x) {
   return x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
          damd_resid_norm_supported(static_cast<int>(x.size(-1)));
@@ -638,7 +647,8 @@ bool resid_norm_supported(const at::Tensor& x) {
 
 // s = x + dropout(branch, p); y = LayerNorm(s).  Returns (s, y, mean, rstd, keep bits).
 std::vector<at::Tensor> resid_norm_fwd(const at::Tensor& x, const at::Tensor& branch, const at::Tensor& gamma,
-                                       const c10::optional<at::Tensor>& beta, double eps, double p, int64_t seed) {
+                                       const c10::optional<at::Tensor>& beta, double eps, double p, int64_t seed,
+                                       const c10::optional<at::Tensor>& seed_t) {
   TORCH_CHECK(resid_norm_supported(x), "resid_norm_fwd: unsupported input");
   TORCH_CHECK(branch.sizes() == x.sizes() && branch.scalar_type() == x.scalar_type() && branch.is_contiguous(),
               "resid_norm_fwd: branch must match x");
@@ -654,7 +664,8 @@ std::vector<at::Tensor> resid_norm_fwd(const at::Tensor& x, const at::Tensor& br
   damd_resid_norm_fwd_launch(x.data_ptr(), branch.data_ptr(), gamma.data_ptr(), bp, sum.data_ptr(), y.data_ptr(),
                              mask.data_ptr<uint8_t>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
                              static_cast<int>(H), static_cast<float>(eps), static_cast<float>(p),
-                             static_cast<uint32_t>(seed), dtype_code(x), dtype_code(gamma), cur_stream());
+                             static_cast<uint32_t>(seed), seed_ptr(seed_t, x), dtype_code(x), dtype_code(gamma),
+                             cur_stream());
   return {sum, y, mean, rstd, mask};
 }
 
@@ -1369,7 +1380,8 @@ const uint8_t* check_kmask(const c10::optional<at::Tensor>& km, const at::Tensor
 }
 
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
-                                 double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed) {
+                                 double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed,
+                                 const c10::optional<at::Tensor>& seed_t) {
   check_attn(q, q, "q");
   check_attn(k, q, "k");
   check_attn(v, q, "v");
@@ -1389,13 +1401,14 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
     damd_attn_fwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), s.data(),
                          static_cast<int>(B), static_cast<int>(H), static_cast<int>(T), static_cast<int>(D),
                          static_cast<float>(scale), causal ? 1 : 0, km, kms, static_cast<uint32_t>(seed),
-                         static_cast<float>(drop_p), cur_stream());
+                         seed_ptr(seed_t, q), static_cast<float>(drop_p), cur_stream());
   return {o, lse};
 }
 
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               const at::Tensor& o, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, bool causal,
-              double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed) {
+              double scale, const c10::optional<at::Tensor>& kmask, double drop_p, int64_t seed,
+              const c10::optional<at::Tensor>& seed_t) {
   check_attn(q, q, "q");
   check_attn(k, q, "k");
   check_attn(v, q, "v");
@@ -1418,7 +1431,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
                          lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr, dq.data_ptr(),
                          dk.data_ptr(), dv.data_ptr(), s.data(), static_cast<int>(B), static_cast<int>(H),
                          static_cast<int>(T), static_cast<int>(D), static_cast<float>(scale), causal ? 1 : 0,
-                         km, kms, static_cast<uint32_t>(seed), static_cast<float>(drop_p), cur_stream());
+                         km, kms, static_cast<uint32_t>(seed), seed_ptr(seed_t, q), static_cast<float>(drop_p),
+                         cur_stream());
 }
 
 // ---------------------------------------------------------------- fused LM loss / bias grad
@@ -1523,10 +1537,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_bias", &gelu_bwd_bias);
   m.def("attn_supported", &attn_supported);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("scale"),
-        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
+        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0, py::arg("seed_t") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"), py::arg("scale"),
-        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
+        py::arg("kmask") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = 0, py::arg("seed_t") = py::none());
   m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
@@ -1539,7 +1553,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_pool_fwd", &bn_pool_fwd);
   m.def("resid_norm_supported", &resid_norm_supported);
-  m.def("resid_norm_fwd", &resid_norm_fwd);
+  m.def("resid_norm_fwd", &resid_norm_fwd, py::arg("x"), py::arg("branch"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("seed_t") = py::none());
   m.def("resid_norm_bwd", &resid_norm_bwd);
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("global_avgpool_bwd", &global_avgpool_bwd);

@@ -58,6 +58,7 @@ struct ResidArgs {
   float keep_scale;     // 1 / (1 - p)
   uint32_t seed;
   uint32_t drop_thresh; // element dropped iff hash < drop_thresh (p * 2^32); 0 = no dropout
+  const int64_t* seedp; // device-side seed (graph-captured steps), or nullptr
 };
 
 __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint64_t e) {
@@ -93,7 +94,7 @@ norm_fwd_kernel(const T* __restrict__ x, const WT* __restrict__ gamma, const WT*
         const uint64_t e0 = static_cast<uint64_t>(row) * H + c;
 #pragma unroll
         for (int k = 0; k < kVecElems; ++k) {
-          const bool keep = ra.drop_thresh == 0u || drop_hash(ra.seed, e0 + k) >= ra.drop_thresh;
+          const bool keep = ra.drop_thresh == 0u || drop_hash(ra.seedp != nullptr ? static_cast<uint32_t>(*ra.seedp) : ra.seed, e0 + k) >= ra.drop_thresh;
           bits |= (keep ? 1u : 0u) << k;
           v[j][k] += keep ? bv[k] * ra.keep_scale : 0.f;
         }
@@ -465,13 +466,15 @@ int damd_resid_norm_supported(int H) {
 
 void damd_resid_norm_fwd_launch(const void* x, const void* branch, const void* gamma, const void* beta, void* sum_out,
                                 void* y, uint8_t* mask, float* mean, float* rstd, int64_t rows, int H, float eps,
-                                float p, uint32_t seed, int x_dtype, int w_dtype, hipStream_t st) {
+                                float p, uint32_t seed, const int64_t* seedp, int x_dtype, int w_dtype,
+                                hipStream_t st) {
   ResidArgs ra;
   ra.branch = branch;
   ra.sum_out = sum_out;
   ra.mask = mask;
   ra.keep_scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   ra.seed = seed;
+  ra.seedp = seedp;
   ra.drop_thresh = p > 0.f ? static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0) : 0u;
   const dim3 grid(static_cast<unsigned>((rows + 3) / 4)), block(kNormThreads);
   const int nv = (H + kWave * kVecElems - 1) / (kWave * kVecElems);

@@ -55,14 +55,16 @@ def key_mask(valid: torch.Tensor) -> torch.Tensor:
     return km
 
 
-def _seed(dropout_p: float) -> int:
-    return int(torch.randint(0, 2**31 - 1, (1,)).item()) if dropout_p > 0 else 0
+def _seed(dropout_p: float, device: torch.device) -> Optional[torch.Tensor]:
+    """The dropout stream of one call: a 1-element int64 GPU tensor the kernels read at run time (an async
+    device RNG draw -- no host round trip, and a graph-captured step draws a fresh seed on every replay)."""
+    return torch.randint(0, 2**31 - 1, (1,), device=device, dtype=torch.int64) if dropout_p > 0 else None
 
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal: bool, scale: float, km=None, dropout_p: float = 0.0, seed: int = 0):
-        o, lse = _ext().attn_fwd(q, k, v, causal, scale, km, dropout_p, seed)
+    def forward(ctx, q, k, v, causal: bool, scale: float, km=None, dropout_p: float = 0.0, seed=None):
+        o, lse = _ext().attn_fwd(q, k, v, causal, scale, km, dropout_p, 0, seed)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale, ctx.km, ctx.dropout_p, ctx.seed = causal, scale, km, dropout_p, seed
         return o
@@ -75,7 +77,7 @@ class _FlashAttnFn(torch.autograd.Function):
         B, H, T, D = q.shape
         g = torch.empty(3, B, T, H, D, dtype=q.dtype, device=q.device).permute(0, 1, 3, 2, 4)
         dq, dk, dv = g[0], g[1], g[2]
-        _ext().attn_bwd(do, q, k, v, o, lse, dq, dk, dv, ctx.causal, ctx.scale, ctx.km, ctx.dropout_p, ctx.seed)
+        _ext().attn_bwd(do, q, k, v, o, lse, dq, dk, dv, ctx.causal, ctx.scale, ctx.km, ctx.dropout_p, 0, ctx.seed)
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -83,9 +85,9 @@ class _QKVFlashAttnFn(torch.autograd.Function):
     """Attention over a packed ``[B, T, 3, H, D]`` tensor; gradient is packed the same way."""
 
     @staticmethod
-    def forward(ctx, qkv, causal: bool, scale: float, dropout_p: float = 0.0, seed: int = 0):
+    def forward(ctx, qkv, causal: bool, scale: float, dropout_p: float = 0.0, seed=None):
         q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3) for i in range(3))
-        o, lse = _ext().attn_fwd(q, k, v, causal, scale, None, dropout_p, seed)
+        o, lse = _ext().attn_fwd(q, k, v, causal, scale, None, dropout_p, 0, seed)
         ctx.save_for_backward(qkv, o, lse)
         ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
         return o
@@ -98,7 +100,7 @@ class _QKVFlashAttnFn(torch.autograd.Function):
         q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3) for i in range(3))
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = (dqkv[:, :, i].permute(0, 2, 1, 3) for i in range(3))
-        _ext().attn_bwd(do, q, k, v, o, lse, dq, dk, dv, ctx.causal, ctx.scale, None, ctx.dropout_p, ctx.seed)
+        _ext().attn_bwd(do, q, k, v, o, lse, dq, dk, dv, ctx.causal, ctx.scale, None, ctx.dropout_p, 0, ctx.seed)
         return dqkv, None, None, None, None
 
 
@@ -113,14 +115,15 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
         raise ValueError("flash_attention needs bf16 GPU tensors [B,H,T,D] with D in {64,128} and a contiguous D")
     if key_padding is not None and (key_padding.dtype != torch.uint8 or key_padding.shape[1] % 64):
         key_padding = key_mask(key_padding)
-    return _FlashAttnFn.apply(q, k, v, causal, float(scale), key_padding, float(dropout_p), _seed(dropout_p))
+    return _FlashAttnFn.apply(q, k, v, causal, float(scale), key_padding, float(dropout_p),
+                              _seed(dropout_p, q.device))
 
 
 def causal_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:
     """``softmax(q k^T / sqrt(d) + causal_mask) v`` for ``[B, H, T, D]`` tensors."""
     if q.is_cuda and _supported(q, k, v):
         return _FlashAttnFn.apply(q, k, v, True, 1.0 / math.sqrt(q.shape[-1]), None, float(dropout_p),
-                                  _seed(dropout_p))
+                                  _seed(dropout_p, q.device))
     if q.is_cuda:
         _configure()
     return F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
@@ -131,7 +134,7 @@ def qkv_attention(qkv: torch.Tensor, causal: bool = True, dropout_p: float = 0.0
     whose memory is ``[B, T, H, D]`` (merging heads afterwards is a free view)."""
     B, T, _, H, D = qkv.shape
     if qkv.is_cuda and qkv.is_contiguous() and qkv.dtype == torch.bfloat16 and D in (64, 128):
-        return _QKVFlashAttnFn.apply(qkv, causal, 1.0 / math.sqrt(D), float(dropout_p), _seed(dropout_p))
+        return _QKVFlashAttnFn.apply(qkv, causal, 1.0 / math.sqrt(D), float(dropout_p), _seed(dropout_p, qkv.device))
     q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
     if qkv.is_cuda:
         _configure()

@@ -57,7 +57,7 @@ class _ResidNormFn(torch.autograd.Function):
         from determined_amd import ops
 
         s, y, mean, rstd, mask = ops.ext().resid_norm_fwd(x.contiguous(), branch.contiguous(), weight.contiguous(),
-                                                          bias, float(eps), float(p), int(seed))
+                                                          bias, float(eps), float(p), 0, seed)
         ctx.save_for_backward(s, weight, mean, rstd, mask)
         ctx.p = float(p)
         ctx.has_bias = bias is not None
@@ -86,7 +86,8 @@ def residual_dropout_layer_norm(x: torch.Tensor, branch: torch.Tensor, norm: "Fu
 
         e = ops.ext()
         if e.resid_norm_supported(x) and branch.dtype == x.dtype and branch.shape == x.shape:
-            seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if p > 0 else 0
+            # device-side seed: no host round trip, a fresh draw on every replay of a captured graph
+            seed = torch.randint(0, 2**31 - 1, (1,), device=x.device, dtype=torch.int64) if p > 0 else None
             return _ResidNormFn.apply(x, branch, norm.weight, norm.bias, norm.eps, p, seed)
     s = x + torch.nn.functional.dropout(branch, p, training=p > 0)
     return s, norm(s)

@@ -37,7 +37,9 @@ def _damd_mask(batch_size: int, q_length: int, kv_length: int, q_offset: int = 0
     am = attention_mask[:, -kv_length:]
     if am.dim() != 2:
         return am
-    if am.shape[1] == kv_length and bool(am.all()):
+    # (inside a graph capture the all-valid shortcut would be a host sync: always pass the mask there)
+    capturing = am.is_cuda and torch.cuda.is_current_stream_capturing()
+    if am.shape[1] == kv_length and not capturing and bool(am.all()):
         return None
     return key_mask(am.bool())
 

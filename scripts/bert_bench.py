@@ -4,7 +4,8 @@ bf16 autocast as the HF Trainer runs it with ``--bf16``): the step the Trainer e
 (forward, loss, backward, optimizer step, zero_grad) timed in a plain loop so the number is not
 diluted by the Trainer's logging.  Variants: ``fused`` (determined_amd.transformers.accelerate +
 fused AdamW), ``fused_bf16w`` (the same with bf16 parameters and fp32 master weights in the fused AdamW:
-no per-step autocast weight casts) and ``stock`` (HF SDPA attention + torch fused AdamW).  One JSON line per variant.
+no per-step autocast weight casts), ``fused_bf16w_graph`` (that step captured once into a hipGraph and
+replayed: determined_amd.utils.graphs.GraphedStep) and ``stock`` (HF SDPA attention + torch fused AdamW).  One JSON line per variant.
 
     python scripts/bert_bench.py [--batch 64] [--seq 128] [--steps 30] [--warmup 10] [--variants fused,stock]
 """
@@ -28,13 +29,14 @@ def build(variant: str, seq: int, dropout: float):
                                   attention_probs_dropout_prob=dropout, attn_implementation="sdpa")
     torch.manual_seed(0)
     model = transformers.BertForMaskedLM(cfg).cuda()
-    if variant in ("fused", "fused_bf16w"):
+    if variant in ("fused", "fused_bf16w", "fused_bf16w_graph"):
         accelerate(model)
         from determined_amd.ops import FusedAdamW
 
-        if variant == "fused_bf16w":  # bf16 parameters, fp32 master weights in the optimizer
+        bf16w = variant != "fused"
+        if bf16w:  # bf16 parameters, fp32 master weights in the optimizer
             model = model.to(torch.bfloat16)
-        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, master_weights=variant == "fused_bf16w")
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, master_weights=bf16w)
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
     return model, opt
@@ -47,7 +49,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dropout", type=float, default=0.1)
-    ap.add_argument("--variants", default="fused,fused_bf16w,stock")
+    ap.add_argument("--variants", default="fused,fused_bf16w,fused_bf16w_graph,stock")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     ids = torch.randint(1000, 30522, (a.batch, a.seq), device="cuda", generator=g)
@@ -57,14 +59,20 @@ def main() -> None:
         model, opt = build(variant, a.seq, a.dropout)
         model.train()
 
+        graphed = variant.endswith("_graph")
+
         def step():
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 loss = model(input_ids=ids, attention_mask=mask, labels=labels).loss
             loss.backward()
             opt.step()
-            opt.zero_grad(set_to_none=True)
+            opt.zero_grad(set_to_none=not graphed)  # a captured step keeps its gradient buffers
             return loss
 
+        if graphed:  # the whole step as one hipGraph (determined_amd.utils.graphs)
+            from determined_amd.utils.graphs import GraphedStep
+
+            step = GraphedStep(step, warmup=3)
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
