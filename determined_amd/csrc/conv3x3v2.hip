@@ -17,7 +17,7 @@
 //     lanes are row-padded (W -> multiple of 16), so a fragment's 16 lanes read 16 consecutive slots of
 //     one image row: the ds_read_b128 lane groups, which mix two chunks (lanes {0-3, 12-15} and {20-27}),
 //     hit 16 distinct bank quads with no swizzle.  (The first version -- 144-byte pixel slots, 8 waves --
-//     spent 23% of its LDS cycles in bank conflicts: profiles/conv3x3v2_pmc_*.)  With W a template
+//     spent 23% of its LDS cycles in bank conflicts: profiles/conv3x3v2_pmc_b2048_1gpu.txt.)  With W a template
 //     constant every tap / k-half offset is an immediate of the ds_read: a B-fragment read costs no VALU;
 //   * 8 waves, 2 per SIMD (256 registers each), every wave a 64-channel x 32- or 64-pixel tile; a tap's
 //     fragments are read after its barrier into one register set, and the other wave on the SIMD
@@ -25,11 +25,15 @@
 //     double-buffered across taps -- halved the LDS reads per MFMA but left the halo staging and epilogue
 //     VALU with no other wave to hide under: 3.4 VALU per MFMA, slower on every layer,
 //     profiles/conv3x3v2_4wave_vs_8wave_b2048_1gpu.txt.)
-// The halo is register-staged (global_load_dwordx4 -> optional BN transform -> ds_write_b128): loaded at
-// the first tap of a 64-channel unit and written into the other halo buffer at tap 5, so five taps of MFMAs
-// cover the HBM latency; the BN prologue's per-channel coefficients are staged in LDS once per launch.
-// Weights stream per tap through a 5-slot LDS ring filled 4 taps ahead by the buffer LDS-DMA
-// (buffer_load_dwordx4 ... lds), XOR-swizzled as in conv_igemm.hip.
+// Halo staging: buffer loads from a per-unit resource whose out-of-range offsets return the zero border
+// (no per-chunk address arithmetic or select).  With a BN prologue the halo is register-staged (load ->
+// transform -> ds_write_b128): loaded at the first tap of a 64-channel unit and written into the other halo
+// buffer at tap 5, so five taps of MFMAs cover the HBM latency; without one it goes straight to LDS by the
+// buffer LDS-DMA.  The BN prologue's per-channel coefficients are staged in LDS once per launch.  Weights
+// stream per tap through a 5-slot LDS ring filled 4 taps ahead by the LDS-DMA, XOR-swizzled as in
+// conv_igemm.hip -- except for 64-channel layers (RES configs), whose whole filter stays resident in LDS:
+// no weight traffic and no per-tap barrier, the waves meet only at unit boundaries.
+// The same file holds the whole-row-tile 3x3 weight gradient (conv3x3v2_wgrad_kernel, below).
 // Work split: persistent blocks (one per CU), each a contiguous run of tiles, so consecutive tiles of an
 // image -- which share two halo rows -- run back to back on the same CU / XCD L2.
 
