@@ -396,6 +396,15 @@ stem_pool_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wk
     const float gv = gamma_bf16 ? bf2f(static_cast<const bf16_t*>(gamma)[ch]) : static_cast<const float*>(gamma)[ch];
     neg[k] = gv < 0.f;
   }
+  // the ring holds pooling KEYS: the conv value, sign-flipped for gamma < 0 channels (exact for bf16), so
+  // the pooling is a plain max with no per-element select; the writer's channels are 16 wave + 4 grp + r
+  uint16_t kflip[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ch = 16 * wave + 4 * grp + r;
+    const float gv = gamma_bf16 ? bf2f(static_cast<const bf16_t*>(gamma)[ch]) : static_cast<const float*>(gamma)[ch];
+    kflip[r] = gv < 0.f ? 0x8000u : 0u;
+  }
   drain_vm();
   float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
   // Iteration h of a band computes conv row h (h < h1) and pools pooled row h / 2 - 1 (even h):
@@ -445,7 +454,7 @@ stem_pool_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wk
             const bf16x8 a = *reinterpret_cast<const bf16x8*>(row + col * kOutRS);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-              const float key = neg[k] ? -bf2f(a.v[k]) : bf2f(a.v[k]);  // exact: a bf16 negated
+              const float key = bf2f(a.v[k]);  // the ring holds keys (see kflip)
               if (key > best[k]) { best[k] = key; arg[k] = kh * 3 + kw; }
             }
           }
@@ -476,6 +485,7 @@ stem_pool_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wk
           const float q = own ? bf2f(v.v[r]) : 0.f;
           st_s[r] += q;
           st_q[r] += q * q;
+          v.v[r] = static_cast<bf16_t>(v.v[r] ^ kflip[r]);  // pooling key
         }
         *reinterpret_cast<bf16x4*>(rs + (16 * t + c) * kOutRS + 16 * wave + 4 * grp) = v;
       }

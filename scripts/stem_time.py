@@ -3,11 +3,14 @@
 stem_pool op (ops/conv.py stem_bn_pool) vs the separate stem-conv + BN/ReLU/max-pool kernels."""
 import argparse
 import json
+import os
+import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
-import determined_amd.ops as ops
-from determined_amd.ops.conv import _StemPoolFn, stem_conv2d
+import determined_amd.ops as ops  # noqa: E402
+from determined_amd.ops.conv import _StemPoolFn, stem_conv2d  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1024)
