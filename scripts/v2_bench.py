@@ -13,7 +13,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.environ.get("DAMD_AB_ROOT", ROOT))  # A/B: another build of the package
 import torch  # noqa: E402
 
 CL = torch.channels_last
